@@ -1,0 +1,314 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s through the FIR -> QuadAmDemod chain on MI355X (BASELINE.json metric).
+
+Default workload (N=1 and every N, weak scaling): BASELINE.json configs[1] ("C2"):
+HackRF-shaped int8 IQ at 20 Msps -> cf32 convert -> 127-tap complex FIR -> QuadAmDemod.
+One step = one second of signal per GPU (20 M IQ samples), inputs resident in HBM.
+The whole chain runs as the fused gfx950 kernel gsdrInt8FirFCAmDemod (== the chain
+gsdrInt8ToNormFloat -> gsdrFirFC -> gsdrQuadAmDemod, bit for bit; tests/test_gpu_parity.py).
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL): the stream is time-sharded.
+In step s rank g owns stream samples [(s*G + g)*L, (s*G + g + 1)*L) and needs the
+preceding T-1 samples as a halo, which live on rank g-1 (rank 0: rank G-1's segment of the
+previous step). Each step therefore does one ring exchange (isend tail -> g+1, irecv
+halo <- g-1, RCCL over xGMI), overlapped with the bulk kernel that needs no halo; a small
+head kernel finishes the first T-1 outputs once the halo has landed.
+
+Other workloads (--workload): c3 (cf32 2^28, 1023 taps, D=10, FIR->AM), c4 (cf32, 1023 taps,
+D=1, FIR->AM), c5 (int8 -> 1023-tap FIR D=10 -> AM -> 255-tap audio FIR D=20).
+
+Output: one JSON line on rank 0 (contract in the task statement) with `roofline` for the
+dominant kernel (HIP events on its stream) and `cpu_baseline` (oracle port, rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "cuda-sdr_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "Msamples/sec through FIR→QuadAmDemod chain at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, spec
+FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md, FP32 vector (packed FMA)
+
+WORKLOADS = {
+    # name: (description, input kind, samples per GPU step, taps, decimation, cutoff, window, fs)
+    "c2": ("C2: HackRF int8 IQ @20 Msps -> cf32 -> 127-tap FC FIR -> QuadAmDemod, 1 s per GPU step",
+           "i8", 20_000_000, 127, 1, 0.1, "hamming", 20e6),
+    "c3": ("C3: wideband cf32 @200 Msps, 2^28 samples -> 1023-tap FC FIR, D=10 -> QuadAmDemod",
+           "c64", 1 << 28, 1023, 10, 0.04, "blackman", 200e6),
+    "c4": ("C4: cf32 stream, 1023-tap FC FIR, D=1 -> QuadAmDemod, 2^26 samples per GPU step",
+           "c64", 1 << 26, 1023, 1, 0.04, "blackman", 1e9),
+    "c5": ("C5: int8 IQ @1 Gsps -> cf32 -> 1023-tap FIR D=10 -> AM -> 255-tap audio FIR D=20, 2^28 per GPU step",
+           "i8", 1 << 28, 1023, 10, 0.04, "blackman", 1e9),
+}
+
+
+def lowpass(num_taps, cutoff, window):
+    n = np.arange(num_taps, dtype=np.float64) - (num_taps - 1) / 2.0
+    h = 2.0 * cutoff * np.sinc(2.0 * cutoff * n)
+    m = np.arange(num_taps, dtype=np.float64)
+    if window == "hamming":
+        w = 0.54 - 0.46 * np.cos(2 * np.pi * m / (num_taps - 1))
+    else:
+        w = 0.42 - 0.5 * np.cos(2 * np.pi * m / (num_taps - 1)) + 0.08 * np.cos(4 * np.pi * m / (num_taps - 1))
+    h = h * w
+    return (h / h.sum()).astype(np.float32)
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return rank, world, local
+
+
+class ShardedChain:
+    """Per-rank state of one time-sharded FIR chain step (see module docstring)."""
+
+    def __init__(self, ops, wl, rank, world, device):
+        desc, kind, L, T, D, cutoff, window, fs = WORKLOADS[wl]
+        self.ops, self.kind, self.L, self.T, self.D, self.fs = ops, kind, L, T, D, fs
+        self.rank, self.world, self.device = rank, world, device
+        self.H = T - 1  # halo samples
+        self.taps = torch.from_numpy(lowpass(T, cutoff, window)).to(device)
+        self.n_out = L // D
+        assert L % D == 0
+        first = (rank * L)  # stream index of this rank's first sample in step 0
+        if kind == "i8":
+            self.buf = torch.empty(2 * (self.H + L), dtype=torch.int8, device=device)
+            self.seg = self.buf[2 * self.H:]
+            ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, first, L, out=self.seg)
+            self.halo = self.buf[: 2 * self.H]
+            self.tail = self.seg[2 * (L - self.H):]
+            self.halo.zero_()
+        else:
+            self.buf = torch.empty(self.H + L, dtype=torch.complex64, device=device)
+            self.seg = self.buf[self.H:]
+            ops.synth_wideband_cf32(0xC3, 0.013, 0.31, first, L, out=self.seg)
+            self.halo = self.buf[: self.H]
+            self.tail = self.seg[L - self.H:]
+            self.halo.zero_()
+        self.out = torch.empty(self.n_out, dtype=torch.float32, device=device)
+        # outputs that need no halo: k*D >= H  ->  k >= ceil(H / D)
+        self.k_split = min(self.n_out, (self.H + D - 1) // D)
+        self.audio = None
+        if wl == "c5":
+            self.audio_taps = torch.from_numpy(lowpass(255, 0.4 / 20, "hamming")).to(device)
+            self.audio_D = 20
+            self.audio_H = 254
+            # the audio FIR's own history carry (AM samples of the previous step's tail)
+            self.audio_buf = torch.zeros(self.audio_H + self.n_out, dtype=torch.float32, device=device)
+            self.audio_out = torch.empty(self.n_out // self.audio_D + 1, dtype=torch.float32, device=device)
+
+    def _fir(self, x, n_out, out):
+        if n_out <= 0:
+            return
+        self.ops.fir(self.taps, x, self.D, n_out, out=out, am=True, int8_iq=(self.kind == "i8"))
+
+    def bulk(self):
+        """Outputs [k_split, n_out): inputs entirely inside this rank's segment."""
+        k0 = self.k_split
+        n = self.n_out - k0
+        start = k0 * self.D - self.H  # offset into seg
+        x = self.seg[2 * start:] if self.kind == "i8" else self.seg[start:]
+        self._fir(x, n, self.out[k0:])
+
+    def head(self):
+        """Outputs [0, k_split): need the halo in front of the segment."""
+        x = self.buf
+        self._fir(x, self.k_split, self.out[: self.k_split])
+
+    def exchange_start(self):
+        if self.world == 1:
+            self.halo.copy_(self.tail)  # ring of one: the previous segment is our own
+            return []
+        nxt = (self.rank + 1) % self.world
+        prv = (self.rank - 1) % self.world
+        ops = [dist.P2POp(dist.isend, self.tail, nxt), dist.P2POp(dist.irecv, self.halo, prv)]
+        return dist.batch_isend_irecv(ops)
+
+    def audio_stage(self):
+        if not hasattr(self, "audio_buf"):
+            return
+        # AM output feeds the 255-tap real audio FIR (D=20) with its own (T_a - 1) carry
+        self.audio_buf[self.audio_H:].copy_(self.out)
+        n = (self.audio_H + self.n_out - 255) // self.audio_D + 1
+        self.ops.fir(self.audio_taps, self.audio_buf, self.audio_D, n, out=self.audio_out[:n])
+        self.audio_buf[: self.audio_H].copy_(self.out[self.n_out - self.audio_H:])
+
+    def step(self, ev=None):
+        reqs = self.exchange_start()
+        if ev is not None:
+            ev[0].record()
+        self.bulk()
+        if ev is not None:
+            ev[1].record()
+        for r in reqs:
+            r.wait()
+        self.head()
+        self.audio_stage()
+
+    def bulk_bytes_flops(self):
+        n = self.n_out - self.k_split
+        n_in = (n - 1) * self.D + self.T
+        in_bytes = n_in * (2 if self.kind == "i8" else 8)
+        return in_bytes + n * 4, n * self.T * 4  # algorithmic bytes; direct-form FC flops
+
+
+def cpu_baseline(wl, seconds_target=8.0):
+    """Oracle port (float32 direct form, all assigned host cores) on a bounded sample."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # noqa: E402  (cpu_baseline leg only)
+    desc, kind, L, T, D, cutoff, window, fs = WORKLOADS[wl]
+    taps = lowpass(T, cutoff, window)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n_out = 1 << 16
+    while True:
+        n_in = (n_out - 1) * D + T
+        if kind == "i8":
+            x = oracle.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, 0, n_in)
+            run = lambda: oracle.chain_i8_fc_am_f32(taps, x, D, n_out, threads)  # noqa: E731
+        else:
+            x = oracle.synth_wideband_cf32(0xC3, 0.013, 0.31, 0, n_in)
+            run = lambda: oracle.chain_fc_am_f32(taps, x, D, n_out, threads)  # noqa: E731
+        run()  # warm
+        t0 = time.perf_counter()
+        run()
+        dt = time.perf_counter() - t0
+        if dt >= seconds_target / 4 or n_out >= (1 << 26):
+            break
+        n_out = int(n_out * min(16.0, max(2.0, (seconds_target / 4) / max(dt, 1e-4))))
+    reps = max(1, int(seconds_target / max(dt, 1e-3)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    dt = (time.perf_counter() - t0) / reps
+    return {
+        "value": (n_out * D) / dt / 1e6,
+        "unit": "Msamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n_out * D} input samples of the {wl} chain (oracle/gsdr_oracle.c float32 direct form, "
+                  f"{threads} threads, mean of {reps} runs)",
+    }
+
+
+def load_traffic(wl):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(wl, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = dist_setup(args.gpus)
+    device = torch.device("cuda", local)
+    from gpusdr import ops
+    chain = ShardedChain(ops, args.workload, rank, world, device)
+
+    for _ in range(args.warmup):
+        chain.step()
+    torch.cuda.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        chain.step(evs[i])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    bytes_, flops = chain.bulk_bytes_flops()
+    achieved_gbs = bytes_ / (kernel_ms * 1e-3) / 1e9
+    achieved_tf = flops / (kernel_ms * 1e-3) / 1e12
+    total_samples = world * chain.L * args.steps
+    value = total_samples / elapsed / 1e6
+
+    if rank == 0:
+        desc = WORKLOADS[args.workload][0]
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.workload)
+        traffic = load_traffic(args.workload)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic splitmix64 + tone generator, generated in HBM)",
+            "config": {
+                "workload": desc,
+                "samples_per_gpu_step": chain.L,
+                "taps": chain.T,
+                "decimation": chain.D,
+                "input": "int8 IQ" if chain.kind == "i8" else "cf32",
+                "parallelism": f"time-shard x{world} (ring halo of {chain.H} samples over RCCL)"
+                if world > 1 else "single GPU (halo = own history carry)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "gsdrInt8FirFCAmDemod (firLdsKernel)" if chain.kind == "i8" else "gsdrFirFCAmDemod",
+                "achieved": achieved_gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved_gbs / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "avg_launch_ms": kernel_ms,
+                "algorithmic_bytes_per_launch": bytes_,
+                "fp32_valu": {"achieved_tflops": achieved_tf, "peak_tflops": FP32_PEAK_TFLOPS,
+                              "frac": achieved_tf / FP32_PEAK_TFLOPS,
+                              "flops_per_launch": flops},
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,489 @@
+// Decimating FIR family for gfx950 (MI355X): gsdrFirFF/FC/CC/CF plus the fused
+// int8->cf32->FIR and FIR->AM-envelope chain kernels.
+//
+// Semantics (reference call sites src/filters/Fir.cpp:229-269, orientation pinned by
+// tests/FirTests.cpp:81-84 and :196-202):
+//     y[k] = sum_{j<T} h[j] * x[k*D + j]
+//
+// Design (see DESIGN.md "FIR kernel"):
+//   * Polyphase split: with j = q*D + p the decimating correlation is a sum over the D
+//     phases p of an undecimated correlation of x_p[m] = x[m*D + p] with h_p[q] = h[q*D + p].
+//   * A 256-thread block owns a tile of 512*WO consecutive outputs. It stages the tile's
+//     input window once from HBM into LDS, phase-major, 8 float2 per 80-byte row (16 B pad:
+//     lane-stride-one-row ds_read_b128 is bank-conflict free).
+//   * Lane t of a wave owns 8 consecutive outputs; for a group of 8 taps it needs rows
+//     (t+g) and (t+g+1) of one phase. The rows slide by one per group, so each group costs
+//     one new row (4 ds_read_b128) for 64 packed FMAs (v_pk_fma_f32, re/im in one op).
+//   * Taps are wave-uniform: read with scalar loads straight from the caller's tap array
+//     (reference layout), so they sit in SGPRs and feed v_pk_fma_f32 as a broadcast operand.
+//   * When the staged window for one wave per output slice would not fit, the 4 waves split
+//     the tap groups instead and their partial sums are added through LDS (fixed order).
+//   * Epilogue through LDS: coalesced 8-byte stores, with the AM envelope (|y|) or the
+//     FF pair de-interleave fused in.
+//   * FF runs as "pseudo-complex": lane element = (x[a+m], x[a+S+m]), i.e. two output
+//     streams S outputs apart share one packed FMA.
+#include "kcommon.h"
+#include "fir_launch.h"
+
+#include <gsdr/gsdr.h>
+#include <gsdr/gsdr_amd.h>
+
+namespace gsdr_amd {
+
+enum InKind : int { kInF32 = 0, kInCF32 = 1, kInI8IQ = 2 };
+
+constexpr int kR = 8;            // consecutive outputs per lane == taps per group
+constexpr int kRowBytes = 80;    // 8 x float2 + 16 B pad
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+constexpr int kWaveOutputs = kWave * kR;  // 512 outputs per wave slice
+
+struct FirArgs {
+  const void* in;
+  const float* taps;
+  void* out;
+  int64_t nOut;
+  int64_t nIn;         // staged reads beyond this are zero
+  int64_t pairOffset;  // FF: input offset between the two packed output streams (= tileOutputs * D)
+  int32_t T;
+  int32_t D;
+  int32_t deff;        // phases that hold taps: min(D, T)
+  int32_t gtot;        // total 8-tap groups over all phases
+  int32_t regionRows;  // LDS rows per phase region
+  int32_t tileOutputs; // outputs per tile (per stream for FF)
+};
+
+template <int MODE, int INK>
+__device__ __forceinline__ f2 loadElement(const FirArgs& a, int64_t gi) {
+  f2 z = {0.0f, 0.0f};
+  if (INK == kInCF32) {
+    if (gi < a.nIn) z = reinterpret_cast<const f2*>(a.in)[gi];
+  } else if (INK == kInI8IQ) {
+    if (gi < a.nIn) {
+      const char2 v = reinterpret_cast<const char2*>(a.in)[gi];
+      z.x = int8ToNorm(v.x);
+      z.y = int8ToNorm(v.y);
+    }
+  } else {  // real input
+    const float* x = reinterpret_cast<const float*>(a.in);
+    if (MODE == kFirFF) {
+      if (gi < a.nIn) z.x = x[gi];
+      if (gi + a.pairOffset < a.nIn) z.y = x[gi + a.pairOffset];
+    } else {  // CF: broadcast the real sample to both lanes of the pair
+      if (gi < a.nIn) z.x = z.y = x[gi];
+    }
+  }
+  return z;
+}
+
+// One group of NV (<= 8) taps against the 16-element window lo[0..7], hi[0..7].
+template <int MODE, int NV>
+__device__ __forceinline__ void firGroup(f2 (&acc)[kR], const f2 (&lo)[kR], const f2 (&hi)[kR],
+                                         const float (&hr)[kR], const float (&hiT)[kR]) {
+#pragma unroll
+  for (int jj = 0; jj < NV; ++jj) {
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const f2 z = (r + jj < kR) ? lo[r + jj] : hi[r + jj - kR];
+      if (MODE == kFirFF || MODE == kFirFC) {
+        const f2 h = {hr[jj], hr[jj]};
+        acc[r] = __builtin_elementwise_fma(h, z, acc[r]);
+      } else if (MODE == kFirCF) {
+        const f2 h = {hr[jj], hiT[jj]};
+        acc[r] = __builtin_elementwise_fma(h, z, acc[r]);  // z = (x, x)
+      } else {  // CC: (hr + i hi)(zr + i zi)
+        const f2 h1 = {hr[jj], hr[jj]};
+        const f2 h2 = {-hiT[jj], hiT[jj]};
+        const f2 zs = {z.y, z.x};
+        acc[r] = __builtin_elementwise_fma(h1, z, acc[r]);
+        acc[r] = __builtin_elementwise_fma(h2, zs, acc[r]);
+      }
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void firGroupDispatch(f2 (&acc)[kR], const f2 (&lo)[kR], const f2 (&hi)[kR],
+                                                 const float (&hr)[kR], const float (&hiT)[kR], int nv) {
+  switch (nv) {
+    case 8: firGroup<MODE, 8>(acc, lo, hi, hr, hiT); break;
+    case 7: firGroup<MODE, 7>(acc, lo, hi, hr, hiT); break;
+    case 6: firGroup<MODE, 6>(acc, lo, hi, hr, hiT); break;
+    case 5: firGroup<MODE, 5>(acc, lo, hi, hr, hiT); break;
+    case 4: firGroup<MODE, 4>(acc, lo, hi, hr, hiT); break;
+    case 3: firGroup<MODE, 3>(acc, lo, hi, hr, hiT); break;
+    case 2: firGroup<MODE, 2>(acc, lo, hi, hr, hiT); break;
+    default: firGroup<MODE, 1>(acc, lo, hi, hr, hiT); break;
+  }
+}
+
+template <int MODE, bool FULL>
+__device__ __forceinline__ void loadTaps(const FirArgs& a, int p, int q0, int nv, float (&hr)[kR], float (&hi)[kR]) {
+#pragma unroll
+  for (int jj = 0; jj < kR; ++jj) {
+    hr[jj] = 0.0f;
+    hi[jj] = 0.0f;
+    if (FULL || jj < nv) {
+      const int idx = (q0 + jj) * a.D + p;
+      if (MODE == kFirFF || MODE == kFirFC) {
+        hr[jj] = a.taps[idx];
+      } else {
+        hr[jj] = a.taps[2 * idx];
+        hi[jj] = a.taps[2 * idx + 1];
+      }
+    }
+  }
+}
+
+// One 8-tap group at (phase p, group gg) against window (lo, hi).
+template <int MODE>
+__device__ __forceinline__ void firStep(const FirArgs& a, f2 (&acc)[kR], const f2 (&lo)[kR], const f2 (&hi)[kR],
+                                        int p, int gg, int qp) {
+  float hr[kR], hiT[kR];
+  const int nv = qp - gg * kR;
+  if (nv >= kR) {
+    loadTaps<MODE, true>(a, p, gg * kR, kR, hr, hiT);
+    firGroup<MODE, kR>(acc, lo, hi, hr, hiT);
+  } else {
+    loadTaps<MODE, false>(a, p, gg * kR, nv, hr, hiT);
+    firGroupDispatch<MODE>(acc, lo, hi, hr, hiT, nv);
+  }
+}
+
+__device__ __forceinline__ void loadRow(f2 (&w)[kR], const uint8_t* rowPtr) {
+  const f4* p = reinterpret_cast<const f4*>(rowPtr);
+#pragma unroll
+  for (int i = 0; i < kR / 2; ++i) {
+    const f4 v = p[i];
+    w[2 * i] = v.xy;
+    w[2 * i + 1] = v.zw;
+  }
+}
+
+// Taps in phase p: q < Qp with q*D + p < T.
+__device__ __forceinline__ int phaseTaps(int T, int D, int p) { return p < T ? (T - p + D - 1) / D : 0; }
+
+template <int MODE, int INK, int EPI, int WO>
+__global__ __launch_bounds__(kThreads) void firLdsKernel(FirArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int WT = kWaves / WO;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int wo = wave % WO;
+  const int wt = wave / WO;
+
+  const int64_t tile = xcdTile(blockIdx.x, gridDim.x);
+  const int64_t tileOut = a.tileOutputs;
+  const int64_t k0 = tile * tileOut * (MODE == kFirFF ? 2 : 1);  // first output of the tile
+  const int64_t inBase = k0 * a.D;
+
+  // ---- stage the input window, phase-major -------------------------------------------
+  const int deff = a.deff;
+  const int regionBytes = a.regionRows * kRowBytes;
+  {
+    const int total = deff * kR * a.regionRows;
+    int p = tid % deff;
+    int m = tid / deff;
+    const int pStep = kThreads % deff;
+    const int mStep = kThreads / deff;
+    for (int n = tid; n < total; n += kThreads) {
+      const f2 z = loadElement<MODE, INK>(a, inBase + (int64_t)m * a.D + p);
+      *reinterpret_cast<f2*>(lds + p * regionBytes + (m >> 3) * kRowBytes + (m & 7) * 8) = z;
+      p += pStep;
+      m += mStep;
+      if (p >= deff) {
+        p -= deff;
+        m += 1;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- this wave's share of the 8-tap groups -------------------------------------------
+  f2 acc[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) acc[r] = f2{0.0f, 0.0f};
+
+  const int fBegin = waveUniform((int)(((int64_t)a.gtot * wt) / WT));
+  const int fEnd = waveUniform((int)(((int64_t)a.gtot * (wt + 1)) / WT));
+  if (fBegin < fEnd) {
+    // locate (phase, group) of fBegin
+    int p = 0;
+    int fAcc = 0;
+    int qp = phaseTaps(a.T, a.D, 0);
+    int gp = (qp + kR - 1) / kR;
+    while (fBegin >= fAcc + gp) {
+      fAcc += gp;
+      ++p;
+      qp = phaseTaps(a.T, a.D, p);
+      gp = (qp + kR - 1) / kR;
+    }
+    int g = fBegin - fAcc;
+    int f = fBegin;
+    const int rowBase = wo * kWave + lane;
+    while (f < fEnd) {
+      const int gEnd = min(gp, g + (fEnd - f));
+      const uint8_t* base = lds + p * regionBytes + (rowBase + g) * kRowBytes;
+      f2 A[kR], B[kR];
+      loadRow(A, base);
+      int gg = g;
+      for (; gg + 2 <= gEnd; gg += 2) {
+        loadRow(B, base + (gg - g + 1) * kRowBytes);
+        firStep<MODE>(a, acc, A, B, p, gg, qp);
+        loadRow(A, base + (gg - g + 2) * kRowBytes);
+        firStep<MODE>(a, acc, B, A, p, gg + 1, qp);
+      }
+      if (gg < gEnd) {
+        loadRow(B, base + (gg - g + 1) * kRowBytes);
+        firStep<MODE>(a, acc, A, B, p, gg, qp);
+      }
+      f += gEnd - g;
+      // next phase with taps
+      do {
+        ++p;
+        qp = phaseTaps(a.T, a.D, p);
+        gp = (qp + kR - 1) / kR;
+      } while (gp == 0 && p < deff);
+      g = 0;
+    }
+  }
+
+  // ---- partial sums -> LDS -> coalesced epilogue --------------------------------------
+  __syncthreads();  // everyone is done reading the staged window
+  f2* red = reinterpret_cast<f2*>(lds);
+  {
+    f4* dst = reinterpret_cast<f4*>(red + wt * tileOut + wo * kWaveOutputs + lane * kR);
+#pragma unroll
+    for (int i = 0; i < kR / 2; ++i) dst[i] = f4{acc[2 * i].x, acc[2 * i].y, acc[2 * i + 1].x, acc[2 * i + 1].y};
+  }
+  __syncthreads();
+
+  for (int j = 2 * tid; j < tileOut; j += 2 * kThreads) {
+    f4 s = *reinterpret_cast<const f4*>(red + j);
+#pragma unroll
+    for (int w = 1; w < WT; ++w) s += *reinterpret_cast<const f4*>(red + w * tileOut + j);
+    const f2 y0 = s.xy;
+    const f2 y1 = s.zw;
+    const int64_t k = k0 + j;
+    if (EPI == kEpiComplex) {
+      f2* o = reinterpret_cast<f2*>(a.out);
+      if (k < a.nOut) o[k] = y0;
+      if (k + 1 < a.nOut) o[k + 1] = y1;
+    } else if (EPI == kEpiAm) {
+      float* o = reinterpret_cast<float*>(a.out);
+      if (k < a.nOut) o[k] = amEnvelope(y0);
+      if (k + 1 < a.nOut) o[k + 1] = amEnvelope(y1);
+    } else {  // kEpiPair (FF): .x -> stream 0, .y -> stream 1 (tileOut further on)
+      float* o = reinterpret_cast<float*>(a.out);
+      const int64_t k2 = k + tileOut;
+      if (k < a.nOut) o[k] = y0.x;
+      if (k + 1 < a.nOut) o[k + 1] = y1.x;
+      if (k2 < a.nOut) o[k2] = y0.y;
+      if (k2 + 1 < a.nOut) o[k2 + 1] = y1.y;
+    }
+  }
+}
+
+// Fallback for windows that do not fit LDS (huge tap counts x decimation): one output per
+// thread, taps and samples read through the caches.
+template <int MODE, int INK, int EPI>
+__global__ __launch_bounds__(kThreads) void firDirectKernel(FirArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (k >= a.nOut) return;
+  f2 acc = {0.0f, 0.0f};
+  const int64_t base = k * a.D;
+  for (int j = 0; j < a.T; ++j) {
+    f2 z;
+    if (INK == kInCF32) {
+      z = reinterpret_cast<const f2*>(a.in)[base + j];
+    } else if (INK == kInI8IQ) {
+      const char2 v = reinterpret_cast<const char2*>(a.in)[base + j];
+      z = f2{int8ToNorm(v.x), int8ToNorm(v.y)};
+    } else {
+      const float x = reinterpret_cast<const float*>(a.in)[base + j];
+      z = f2{x, x};
+    }
+    if (MODE == kFirFF || MODE == kFirFC) {
+      acc = __builtin_elementwise_fma(f2{a.taps[j], a.taps[j]}, z, acc);
+    } else if (MODE == kFirCF) {
+      acc = __builtin_elementwise_fma(f2{a.taps[2 * j], a.taps[2 * j + 1]}, z, acc);
+    } else {
+      const float hr = a.taps[2 * j], hi = a.taps[2 * j + 1];
+      acc = __builtin_elementwise_fma(f2{hr, hr}, z, acc);
+      acc = __builtin_elementwise_fma(f2{-hi, hi}, f2{z.y, z.x}, acc);
+    }
+  }
+  if (EPI == kEpiComplex) {
+    reinterpret_cast<f2*>(a.out)[k] = acc;
+  } else if (EPI == kEpiAm) {
+    reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc);
+  } else {
+    reinterpret_cast<float*>(a.out)[k] = acc.x;  // FF direct: both lanes hold the same value
+  }
+}
+
+// ---- host side --------------------------------------------------------------------------
+
+namespace {
+
+struct DevicePush {
+  int prev = -1;
+  bool ok = true;
+  explicit DevicePush(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DevicePush() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+constexpr size_t kLdsSoftLimit = 64 * 1024;
+constexpr size_t kLdsHardLimit = 160 * 1024;
+
+template <typename K>
+hipError_t ensureLds(K kernel, size_t bytes) {
+  if (bytes <= 64 * 1024) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes);
+}
+
+template <int MODE, int INK, int EPI, int WO>
+hipError_t launchLds(FirArgs a, size_t lds, hipStream_t stream) {
+  const int64_t perTile = (int64_t)a.tileOutputs * (MODE == kFirFF ? 2 : 1);
+  const int64_t tiles = (a.nOut + perTile - 1) / perTile;
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  auto kernel = firLdsKernel<MODE, INK, EPI, WO>;
+  hipError_t e = ensureLds(kernel, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)tiles), dim3(kThreads), lds, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+FirPlanShape planFirShape(size_t tapCount, size_t decimation) {
+  FirPlanShape s{};
+  const size_t D = decimation == 0 ? 1 : decimation;
+  const size_t T = tapCount;
+  s.decimation = D;
+  s.deff = D < T ? D : T;
+  size_t gtot = 0, gmax = 0;
+  for (size_t p = 0; p < s.deff; ++p) {
+    const size_t q = (T - p + D - 1) / D;
+    const size_t g = (q + kR - 1) / kR;
+    gtot += g;
+    gmax = g > gmax ? g : gmax;
+  }
+  s.gtot = gtot;
+  s.gmax = gmax;
+  s.waveOutputSlices = 0;
+  for (int wo : {4, 2, 1}) {
+    const size_t rows = (size_t)kWave * wo + gmax;
+    const size_t staging = s.deff * rows * kRowBytes;
+    const size_t reduce = (size_t)kWaves * kWaveOutputs * 8;  // WT * tileOutputs * sizeof(float2)
+    const size_t lds = staging > reduce ? staging : reduce;
+    if (lds <= kLdsSoftLimit || (wo == 1 && lds <= kLdsHardLimit)) {
+      s.waveOutputSlices = wo;
+      s.regionRows = rows;
+      s.ldsBytes = lds;
+      s.tileOutputs = (size_t)kWaveOutputs * wo;
+      break;
+    }
+  }
+  return s;
+}
+
+template <int MODE, int INK, int EPI>
+hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t decimation, void* out,
+                     size_t nOut, int32_t device, hipStream_t stream) {
+  if (nOut == 0) return hipSuccess;
+  if (in == nullptr || taps == nullptr || out == nullptr || tapCount == 0) return hipErrorInvalidValue;
+  if (tapCount > 0x7fffffff || decimation > 0x7fffffff) return hipErrorInvalidValue;
+  DevicePush push(device);
+  if (!push.ok) return hipErrorInvalidDevice;
+
+  const FirPlanShape s = planFirShape(tapCount, decimation);
+  FirArgs a{};
+  a.in = in;
+  a.taps = taps;
+  a.out = out;
+  a.nOut = (int64_t)nOut;
+  a.nIn = (int64_t)(nOut - 1) * (int64_t)s.decimation + (int64_t)tapCount;
+  a.T = (int32_t)tapCount;
+  a.D = (int32_t)s.decimation;
+  a.deff = (int32_t)s.deff;
+  a.gtot = (int32_t)s.gtot;
+
+  if (s.waveOutputSlices == 0) {
+    a.tileOutputs = kThreads;
+    const int64_t blocks = ((int64_t)nOut + kThreads - 1) / kThreads;
+    hipLaunchKernelGGL((firDirectKernel<MODE, INK, EPI>), dim3((unsigned)blocks), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+  }
+  a.regionRows = (int32_t)s.regionRows;
+  a.tileOutputs = (int32_t)s.tileOutputs;
+  a.pairOffset = (int64_t)s.tileOutputs * a.D;
+  switch (s.waveOutputSlices) {
+    case 4: return launchLds<MODE, INK, EPI, 4>(a, s.ldsBytes, stream);
+    case 2: return launchLds<MODE, INK, EPI, 2>(a, s.ldsBytes, stream);
+    default: return launchLds<MODE, INK, EPI, 1>(a, s.ldsBytes, stream);
+  }
+}
+
+}  // namespace gsdr_amd
+
+using namespace gsdr_amd;
+
+extern "C" {
+
+hipError_t gsdrFirFF(size_t decimation, const float* taps, size_t tapCount, const float* input, float* output,
+                     size_t outputCount, int32_t device, hipStream_t stream) {
+  return launchFir<kFirFF, kInF32, kEpiPair>(input, taps, tapCount, decimation, output, outputCount, device, stream);
+}
+
+hipError_t gsdrFirFC(size_t decimation, const float* taps, size_t tapCount, const hipFloatComplex* input,
+                     hipFloatComplex* output, size_t outputCount, int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInCF32, kEpiComplex>(input, taps, tapCount, decimation, output, outputCount, device,
+                                                 stream);
+}
+
+hipError_t gsdrFirCC(size_t decimation, const hipFloatComplex* taps, size_t tapCount, const hipFloatComplex* input,
+                     hipFloatComplex* output, size_t outputCount, int32_t device, hipStream_t stream) {
+  return launchFir<kFirCC, kInCF32, kEpiComplex>(input, reinterpret_cast<const float*>(taps), tapCount, decimation,
+                                                 output, outputCount, device, stream);
+}
+
+hipError_t gsdrFirCF(size_t decimation, const hipFloatComplex* taps, size_t tapCount, const float* input,
+                     hipFloatComplex* output, size_t outputCount, int32_t device, hipStream_t stream) {
+  return launchFir<kFirCF, kInF32, kEpiComplex>(input, reinterpret_cast<const float*>(taps), tapCount, decimation,
+                                                output, outputCount, device, stream);
+}
+
+hipError_t gsdrFirFCAmDemod(size_t decimation, const float* taps, size_t tapCount, const hipFloatComplex* input,
+                            float* output, size_t outputCount, int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInCF32, kEpiAm>(input, taps, tapCount, decimation, output, outputCount, device, stream);
+}
+
+hipError_t gsdrInt8FirFC(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
+                         hipFloatComplex* output, size_t outputCount, int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInI8IQ, kEpiComplex>(inputIq, taps, tapCount, decimation, output, outputCount, device,
+                                                 stream);
+}
+
+hipError_t gsdrInt8FirFCAmDemod(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
+                                float* output, size_t outputCount, int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInI8IQ, kEpiAm>(inputIq, taps, tapCount, decimation, output, outputCount, device,
+                                            stream);
+}
+
+hipError_t gsdrFirCCAmDemod(size_t decimation, const hipFloatComplex* taps, size_t tapCount,
+                            const hipFloatComplex* input, float* output, size_t outputCount, int32_t device,
+                            hipStream_t stream) {
+  return launchFir<kFirCC, kInCF32, kEpiAm>(input, reinterpret_cast<const float*>(taps), tapCount, decimation,
+                                            output, outputCount, device, stream);
+}
+
+}  // extern "C"

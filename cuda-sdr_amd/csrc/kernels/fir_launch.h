@@ -1,0 +1,25 @@
+// Host-side FIR launch geometry shared by the kernel launchers and the filter layer.
+#pragma once
+
+#include <stddef.h>
+
+namespace gsdr_amd {
+
+enum FirMode : int { kFirFF = 0, kFirFC = 1, kFirCC = 2, kFirCF = 3 };
+enum FirEpilogue : int { kEpiComplex = 0, kEpiPair = 1, kEpiAm = 2 };
+
+struct FirPlanShape {
+  size_t decimation;        // clamped to >= 1
+  size_t deff;              // phases that carry taps: min(decimation, tapCount)
+  size_t gtot;              // 8-tap groups summed over phases
+  size_t gmax;              // 8-tap groups in the longest phase
+  int waveOutputSlices;     // WO: 4, 2 or 1 waves along the outputs; 0 = direct (no-LDS) kernel
+  size_t regionRows;        // LDS rows per phase region (64*WO + gmax)
+  size_t ldsBytes;          // dynamic LDS per block
+  size_t tileOutputs;       // outputs per block tile (per stream for FF)
+};
+
+// Geometry the LDS kernel uses for a (tapCount, decimation) pair.
+FirPlanShape planFirShape(size_t tapCount, size_t decimation);
+
+}  // namespace gsdr_amd

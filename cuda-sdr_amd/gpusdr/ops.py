@@ -1,0 +1,140 @@
+"""Tensor-level wrappers over the gsdr C-ABI (include/gsdr/*.h).
+
+Plumbing only: torch provides device memory and the current HIP stream; every call goes
+straight to a hand-written gfx950 kernel in libgpusdrpipeline.so. Each wrapper mirrors one
+reference entry point (argument meaning and the FIR count rule of src/filters/Fir.cpp).
+"""
+from __future__ import annotations
+
+import torch
+
+from ._native import check, lib
+
+
+def _stream(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _dev(t: torch.Tensor) -> int:
+    return t.device.index if t.device.index is not None else torch.cuda.current_device()
+
+
+def _require(t: torch.Tensor, dtype, name: str):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def fir_output_count(num_inputs: int, tap_count: int, decimation: int) -> int:
+    """Fir.cpp:178-186 with the size_t wrap guarded."""
+    d = max(1, int(decimation))
+    if tap_count == 0 or num_inputs < tap_count:
+        return 0
+    return (num_inputs - (tap_count - 1)) // d
+
+
+_FIR_ENTRY = {
+    # (taps complex, input kind, am epilogue) -> entry point
+    (False, "f32", False): "gsdrFirFF",
+    (False, "c64", False): "gsdrFirFC",
+    (True, "c64", False): "gsdrFirCC",
+    (True, "f32", False): "gsdrFirCF",
+    (False, "c64", True): "gsdrFirFCAmDemod",
+    (True, "c64", True): "gsdrFirCCAmDemod",
+    (False, "i8iq", False): "gsdrInt8FirFC",
+    (False, "i8iq", True): "gsdrInt8FirFCAmDemod",
+}
+
+
+def fir(taps: torch.Tensor, x: torch.Tensor, decimation: int = 1, num_outputs: int | None = None,
+        out: torch.Tensor | None = None, am: bool = False, int8_iq: bool = False) -> torch.Tensor:
+    """y[k] = sum_j taps[j] * x[k*D + j] on the GPU.
+
+    taps: float32 (real) or complex64, device.  x: float32, complex64, or (int8_iq=True) int8
+    interleaved I/Q.  am=True fuses the QuadAmDemod envelope (float32 output)."""
+    taps_c = taps.dtype == torch.complex64
+    _require(taps, torch.complex64 if taps_c else torch.float32, "taps")
+    if int8_iq:
+        _require(x, torch.int8, "x")
+        kind, n_in = "i8iq", x.numel() // 2
+    elif x.dtype == torch.complex64:
+        _require(x, torch.complex64, "x")
+        kind, n_in = "c64", x.numel()
+    else:
+        _require(x, torch.float32, "x")
+        kind, n_in = "f32", x.numel()
+    key = (taps_c, kind, am)
+    if key not in _FIR_ENTRY:
+        raise ValueError(f"unsupported FIR combination {key}")
+    d = max(1, int(decimation))
+    T = taps.numel()
+    if num_outputs is None:
+        num_outputs = fir_output_count(n_in, T, d)
+    if num_outputs > 0 and (num_outputs - 1) * d + T > n_in:
+        raise ValueError("input too short for the requested outputs")
+    out_dtype = torch.float32 if (am or (not taps_c and kind == "f32")) else torch.complex64
+    if out is None:
+        out = torch.empty(num_outputs, dtype=out_dtype, device=x.device)
+    else:
+        _require(out, out_dtype, "out")
+        if out.numel() < num_outputs:
+            raise ValueError("out too small")
+    if num_outputs == 0:
+        return out
+    fn = getattr(lib(), _FIR_ENTRY[key])
+    check(fn(d, taps.data_ptr(), T, x.data_ptr(), out.data_ptr(), num_outputs, _dev(x), _stream(x)), fn.__name__)
+    return out
+
+
+def quad_am_demod(z: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    _require(z, torch.complex64, "z")
+    if out is None:
+        out = torch.empty(z.numel(), dtype=torch.float32, device=z.device)
+    check(lib().gsdrQuadAmDemod(z.data_ptr(), out.data_ptr(), z.numel(), _dev(z), _stream(z)), "gsdrQuadAmDemod")
+    return out
+
+
+def int8_to_norm_float(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    _require(x, torch.int8, "x")
+    if out is None:
+        out = torch.empty(x.numel(), dtype=torch.float32, device=x.device)
+    check(lib().gsdrInt8ToNormFloat(x.data_ptr(), out.data_ptr(), x.numel(), _dev(x), _stream(x)),
+          "gsdrInt8ToNormFloat")
+    return out
+
+
+def float_to_int8(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    _require(x, torch.float32, "x")
+    if out is None:
+        out = torch.empty(x.numel(), dtype=torch.int8, device=x.device)
+    check(lib().gsdrFloatToInt8(x.data_ptr(), out.data_ptr(), x.numel(), _dev(x), _stream(x)), "gsdrFloatToInt8")
+    return out
+
+
+def cosine(phi_begin: float, phi_end: float, n: int, complex_out: bool, device="cuda") -> torch.Tensor:
+    dt = torch.complex64 if complex_out else torch.float32
+    out = torch.empty(n, dtype=dt, device=device)
+    fn = lib().gsdrCosineC if complex_out else lib().gsdrCosineF
+    check(fn(phi_begin, phi_end, out.data_ptr(), n, _dev(out), _stream(out)), fn.__name__)
+    return out
+
+
+def synth_iq_int8(seed: int, fs: float, am_hz: float, carrier_hz: float, first: int, n: int,
+                  out: torch.Tensor | None = None, device="cuda") -> torch.Tensor:
+    if out is None:
+        out = torch.empty(2 * n, dtype=torch.int8, device=device)
+    check(lib().gsdrSynthIqInt8(seed, fs, am_hz, carrier_hz, first, out.data_ptr(), n, _dev(out), _stream(out)),
+          "gsdrSynthIqInt8")
+    return out
+
+
+def synth_wideband_cf32(seed: int, f1: float, f2: float, first: int, n: int,
+                        out: torch.Tensor | None = None, device="cuda") -> torch.Tensor:
+    if out is None:
+        out = torch.empty(n, dtype=torch.complex64, device=device)
+    check(lib().gsdrSynthWidebandCf32(seed, f1, f2, first, out.data_ptr(), n, _dev(out), _stream(out)),
+          "gsdrSynthWidebandCf32")
+    return out

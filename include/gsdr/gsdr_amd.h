@@ -1,0 +1,63 @@
+/*
+ * gsdr_amd.h - MI355X-only extensions to the gsdr kernel ABI.
+ *
+ * Fused chain kernels for the FIR -> QuadAmDemod hot path (BASELINE.json north star).
+ * They compute exactly what the corresponding chain of reference entry points computes
+ * (same arithmetic per stage, intermediates kept on chip instead of in HBM):
+ *
+ *   gsdrInt8FirFC          == gsdrInt8ToNormFloat -> gsdrFirFC
+ *   gsdrInt8FirFCAmDemod   == gsdrInt8ToNormFloat -> gsdrFirFC -> gsdrQuadAmDemod
+ *   gsdrFirFCAmDemod       == gsdrFirFC -> gsdrQuadAmDemod
+ *   gsdrFirCCAmDemod       == gsdrFirCC -> gsdrQuadAmDemod
+ *
+ * `inputIq` is interleaved int8 I,Q (2 bytes per complex sample); `outputCount` counts
+ * FIR outputs exactly as in gsdr.h, so the caller supplies
+ * (outputCount - 1) * decimation + tapCount complex input samples.
+ */
+#ifndef GSDR_GSDR_AMD_H
+#define GSDR_GSDR_AMD_H
+
+#include <gsdr/gsdr.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+GSDR_API hipError_t gsdrInt8FirFC(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
+                                  hipFloatComplex* output, size_t outputCount, int32_t device, hipStream_t stream);
+GSDR_API hipError_t gsdrInt8FirFCAmDemod(size_t decimation, const float* taps, size_t tapCount,
+                                         const int8_t* inputIq, float* output, size_t outputCount, int32_t device,
+                                         hipStream_t stream);
+GSDR_API hipError_t gsdrFirFCAmDemod(size_t decimation, const float* taps, size_t tapCount,
+                                     const hipFloatComplex* input, float* output, size_t outputCount, int32_t device,
+                                     hipStream_t stream);
+GSDR_API hipError_t gsdrFirCCAmDemod(size_t decimation, const hipFloatComplex* taps, size_t tapCount,
+                                     const hipFloatComplex* input, float* output, size_t outputCount, int32_t device,
+                                     hipStream_t stream);
+
+/*
+ * Deterministic synthetic sources for the benchmark configurations.
+ * Sample n (absolute stream index firstSample + i) depends only on (seed, n), so a
+ * time-sharded stream is generated shard by shard with no communication.
+ *
+ * C2-style HackRF IQ (int8, 2 bytes per sample):
+ *   s[n] = 100 (1 + 0.5 cos(2 pi fAm n / fs)) exp(j 2 pi fCarrier n / fs) + u[n],
+ *   u = uniform in [-3, 3) per component from splitmix64(seed ^ (2n + c)),
+ *   rounded half away from zero, clipped to [-127, 127].
+ * C3-style wideband cf32:
+ *   x[n] = exp(j 2 pi f1 n) + 0.5 exp(j 2 pi f2 n) + 0.01 (u_r + j u_i),  u in [-1, 1),
+ *   f1, f2 in cycles per sample.
+ * Phases are reduced in double precision (n mod period) before the float trig.
+ */
+GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
+                                    uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,
+                                    hipStream_t stream);
+GSDR_API hipError_t gsdrSynthWidebandCf32(uint64_t seed, double f1, double f2Cycles, uint64_t firstSample,
+                                          hipFloatComplex* output, size_t numSamples, int32_t device,
+                                          hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSDR_GSDR_AMD_H */

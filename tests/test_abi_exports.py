@@ -1,0 +1,54 @@
+"""The C-ABI library builds, loads without a GPU and exports every symbol include/ declares."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "cuda-sdr_amd", "lib", "libgpusdrpipeline.so")
+EXPORT_RE = re.compile(r"^\s*(?:GSDR_API|GSDR_CONV_API|GS_EXPORT)\b[^(]*?\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", re.M)
+
+
+def declared_symbols():
+    names = set()
+    for root, _, files in os.walk(os.path.join(REPO, "include")):
+        for f in files:
+            if f.endswith(".h"):
+                with open(os.path.join(root, f)) as fh:
+                    names.update(EXPORT_RE.findall(fh.read()))
+    return names
+
+
+def exported_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], check=True, capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if len(line.split()) >= 3}
+
+
+@pytest.fixture(scope="module")
+def built():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(REPO, "cuda-sdr_amd")], check=True)
+    return LIB
+
+
+def test_every_declared_symbol_is_exported(built):
+    declared = declared_symbols()
+    assert {"gsdrFirFC", "gsdrQuadAmDemod", "gsdrInt8ToNormFloat"} <= declared
+    missing = declared - exported_symbols()
+    assert not missing, sorted(missing)
+
+
+def test_library_is_gfx950_code(built):
+    with open(built, "rb") as f:
+        blob = f.read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"--gfx942" not in blob and b"--gfx90a" not in blob
+
+
+def test_library_loads_without_gpu(built):
+    code = ("import ctypes,sys; L=ctypes.CDLL(sys.argv[1]); "
+            "assert L.gsdrFirFC and L.gsdrInt8FirFCAmDemod; print('ok')")
+    r = subprocess.run([sys.executable, "-c", code, built], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr

@@ -1,0 +1,242 @@
+"""GPU parity: the gfx950 kernels (through the gsdr C-ABI) against the CPU oracle.
+
+Tolerances (BASELINE.json north star):
+  * FIR / FIR->AM: per element |y - y64| <= 1e-6 * sum_j |h_j||x_kD+j| (the float64 oracle's
+    bound), plus relative L2 <= 1e-6.
+  * int8 -> float and the AM envelope: bit-exact against the oracle's identical expression.
+  * fused chains: bit-exact against the unfused chain of reference entry points.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FIR_TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def ops():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from gpusdr import ops as _ops
+    return _ops
+
+
+def _dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _host(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def _check_fir(y, y64, bound, what):
+    err = np.abs(y.astype(np.complex128) - y64)
+    assert np.all(err <= FIR_TOL * bound + 1e-30), (what, float(np.max(err / (bound + 1e-30))))
+    den = np.linalg.norm(y64)
+    if den > 0:
+        assert np.linalg.norm(y - y64) / den <= FIR_TOL, what
+
+
+def test_fir_golden_all_variants(ops, golden_dir):
+    g = np.load(os.path.join(golden_dir, "fir_golden.npz"))
+    keys = sorted({k.rsplit("_", 1)[0] for k in g.files})
+    for key in keys:
+        D = int(key.split("_D")[1])
+        taps, x, y64, bound = g[key + "_taps"], g[key + "_x"], g[key + "_y"], g[key + "_bound"]
+        y = _host(ops.fir(_dev(taps), _dev(x), D, len(y64)))
+        _check_fir(y, y64, bound, key)
+
+
+def test_fir_kats(ops):
+    # FirTests.cpp:81-84 and :196-202 (full reads; chunked reads are in test_filter_graph)
+    x = np.array([0.1 + 0.2j, 0.3 + 0.4j, 0.5 + 0.6j, 0.7 + 0.8j, 0.9 + 0.9j], dtype=np.complex64)
+    y = _host(ops.fir(_dev(np.array([0.5, 1.0], np.float32)), _dev(x), 2))
+    assert np.allclose(y, [0.35 + 0.5j, 0.95 + 1.1j], atol=1e-6)
+    x = np.array([0.1 + 0.2j, 0.3 + 0.4j, 0.5 + 0.6j, 0.7 + 0.8j] * 2, dtype=np.complex64)
+    y = _host(ops.fir(_dev(np.array([0.5, 1.0, 0.25], np.float32)), _dev(x), 2))
+    assert np.allclose(y, [0.475 + 0.65j, 0.975 + 1.15j, 0.475 + 0.65j], atol=1e-6)
+
+
+RAGGED = [
+    # (T, D, nOut)
+    (1, 1, 1), (2, 2, 2), (3, 2, 7), (8, 1, 511), (9, 1, 513), (63, 1, 2047), (127, 1, 2049),
+    (127, 3, 1000), (1023, 10, 1537), (1023, 1, 4099), (17, 64, 300), (3, 16, 100), (2000, 7, 777),
+    (4096, 1, 3000), (20000, 10, 300),  # the last one exceeds LDS: direct fallback kernel
+]
+
+
+@pytest.mark.parametrize("T,D,n_out", RAGGED)
+@pytest.mark.parametrize("mode", ["FF", "FC", "CC", "CF"])
+def test_fir_ragged(ops, orc, T, D, n_out, mode):
+    rng = np.random.default_rng(T * 131 + D * 7 + n_out)
+    n_in = (n_out - 1) * D + T
+    taps = rng.standard_normal(T).astype(np.float32) / np.sqrt(T)
+    if mode[0] == "C":
+        taps = (taps + 1j * rng.standard_normal(T).astype(np.float32) / np.sqrt(T)).astype(np.complex64)
+    if mode[1] == "C":
+        x = (rng.standard_normal(n_in) + 1j * rng.standard_normal(n_in)).astype(np.complex64)
+    else:
+        x = rng.standard_normal(n_in).astype(np.float32)
+    y64, bound = orc.fir_f64(taps, x, D, n_out)
+    y = _host(ops.fir(_dev(taps), _dev(x), D, n_out))
+    _check_fir(y, y64, bound, (mode, T, D, n_out))
+
+
+def test_fir_misaligned_pointers(ops, orc):
+    import torch
+    rng = np.random.default_rng(11)
+    T, D, n_out = 127, 2, 3001
+    taps = rng.standard_normal(T).astype(np.float32)
+    x = (rng.standard_normal((n_out - 1) * D + T + 3) + 1j * rng.standard_normal((n_out - 1) * D + T + 3))
+    x = x.astype(np.complex64)
+    xd = _dev(x)
+    out = torch.zeros(n_out + 3, dtype=torch.complex64, device="cuda")
+    for off in (1, 3):
+        ops.fir(_dev(taps), xd[off:], D, n_out, out=out[off:off + n_out])
+        y64, bound = orc.fir_f64(taps, x[off:], D, n_out)
+        _check_fir(_host(out)[off:off + n_out], y64, bound, off)
+
+
+def test_fir_does_not_write_past_outputs(ops):
+    import torch
+    T, D, n_out = 63, 1, 777
+    x = torch.randn(n_out - 1 + T, dtype=torch.complex64, device="cuda")
+    taps = torch.randn(T, device="cuda")
+    out = torch.full((n_out + 1000,), 7.0 + 7.0j, dtype=torch.complex64, device="cuda")
+    ops.fir(taps, x, D, n_out, out=out[:n_out])
+    tail = _host(out)[n_out:]
+    assert np.all(tail == np.complex64(7 + 7j))
+
+
+def test_fir_inf_sample_stays_local(ops, orc):
+    """A non-finite sample may only reach outputs whose taps touch it (no zero-padded tap x inf)."""
+    T, D, n_out = 100, 3, 400
+    x = np.ones((n_out - 1) * D + T, dtype=np.complex64)
+    bad = 600
+    x[bad] = np.inf
+    taps = np.full(T, 0.01, dtype=np.float32)
+    y = _host(ops.fir(_dev(taps), _dev(x), D, n_out))
+    touched = np.array([(k * D <= bad < k * D + T) for k in range(n_out)])
+    assert np.all(np.isfinite(y[~touched]))
+    assert np.all(~np.isfinite(y[touched]))
+
+
+def test_int8_to_float_all_codes_bit_exact(ops, orc, golden_dir):
+    g = np.load(os.path.join(golden_dir, "int8_golden.npz"))
+    codes = np.tile(g["codes"], 9)  # 2304 elements: vector path + tail
+    out = _host(ops.int8_to_norm_float(_dev(codes)))
+    assert out.tobytes() == np.tile(g["table"], 9).tobytes()
+    for off in (1, 5, 15):  # misaligned input -> scalar path
+        out = _host(ops.int8_to_norm_float(_dev(codes)[off:]))
+        assert out.tobytes() == orc.int8_to_float(codes[off:]).tobytes()
+
+
+def test_am_demod_bit_exact(ops, orc, golden_dir):
+    g = np.load(os.path.join(golden_dir, "am_golden.npz"))
+    z = g["z"]
+    out = _host(ops.quad_am_demod(_dev(z)))
+    assert out.tobytes() == orc.quad_am_demod(z).tobytes()
+    out = _host(ops.quad_am_demod(_dev(z)[1:]))  # odd start: scalar path
+    assert out.tobytes() == orc.quad_am_demod(z[1:]).tobytes()
+
+
+@pytest.mark.parametrize("T,D", [(127, 1), (1023, 10), (255, 20), (5, 1)])
+def test_fused_chains_match_unfused_bit_exact(ops, orc, T, D):
+    """int8 -> FIR -> AM in one kernel == gsdrInt8ToNormFloat -> gsdrFirFC -> gsdrQuadAmDemod."""
+    import torch
+    rng = np.random.default_rng(T + D)
+    n_out = 5000
+    n_in = (n_out - 1) * D + T
+    iq = rng.integers(-128, 128, size=2 * n_in).astype(np.int8)
+    taps = orc.lowpass_taps(T, 0.2 / D if D > 1 else 0.1)
+    iq_d, taps_d = _dev(iq), _dev(taps)
+    xf = ops.int8_to_norm_float(iq_d).view(torch.complex64)
+    y_unfused = ops.fir(taps_d, xf, D, n_out)
+    am_unfused = ops.quad_am_demod(y_unfused)
+    y_fused = ops.fir(taps_d, iq_d, D, n_out, int8_iq=True)
+    am_fused = ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=True)
+    am_fir_fused = ops.fir(taps_d, xf, D, n_out, am=True)
+    assert _host(y_fused).tobytes() == _host(y_unfused).tobytes()
+    assert _host(am_fused).tobytes() == _host(am_unfused).tobytes()
+    assert _host(am_fir_fused).tobytes() == _host(am_unfused).tobytes()
+    # and against the float64 oracle
+    x = orc.int8_to_float(iq).view(np.complex64)
+    y64, bound = orc.fir_f64(taps, x, D, n_out)
+    assert np.all(np.abs(_host(am_fused) - np.abs(y64)) <= FIR_TOL * bound + 1e-30)
+
+
+def test_cosine_sources(ops, orc):
+    # CosineSourceTests.cpp:8-56 KAT plus the oracle over a longer run
+    delta = np.float32(2.0 * np.pi * 1.0 / 100.0)
+    z = _host(ops.cosine(0.0, float(np.float32(104) * delta), 104, True))
+    theta = np.arange(101, dtype=np.float32) * np.float32(0.01) * np.float32(np.pi) * np.float32(2)
+    assert np.all(np.abs(z[:101].real - np.cos(theta)) < 1e-4)
+    assert np.all(np.abs(z[:101].imag - np.sin(theta)) < 1e-4)
+    f = _host(ops.cosine(0.25, 1000.25, 1 << 16, False))
+    assert np.max(np.abs(f - orc.cosine_f(0.25, 1000.25, 1 << 16))) < 2e-5
+
+
+def test_synth_sources_match_oracle(ops, orc):
+    n = 100_000
+    a = _host(ops.synth_iq_int8(0x5EED, 20e6, 1e3, 1.5e6, 12345, n))
+    b = orc.synth_iq_int8(0x5EED, 20e6, 1e3, 1.5e6, 12345, n)
+    diff = np.abs(a.astype(np.int32) - b.astype(np.int32))
+    assert diff.max() <= 1 and np.mean(diff == 0) > 0.999
+    w = _host(ops.synth_wideband_cf32(0xC3, 0.013, 0.31, 777, n))
+    assert np.max(np.abs(w - orc.synth_wideband_cf32(0xC3, 0.013, 0.31, 777, n))) < 1e-5
+
+
+def test_large_chain_sampled_parity(ops, orc):
+    """C3-sized stream (2^24 cf32, 1023 taps, D=10): spot-check 2000 outputs against float64."""
+    import torch
+    n_in = 1 << 24
+    T, D = 1023, 10
+    taps = orc.lowpass_taps(T, 0.04, "blackman")
+    x = ops.synth_wideband_cf32(0xC3, 0.013, 0.31, 0, n_in)
+    n_out = ops.fir_output_count(n_in, T, D)
+    am = ops.fir(_dev(taps), x, D, n_out, am=True)
+    rng = np.random.default_rng(5)
+    ks = np.sort(rng.choice(n_out, 2000, replace=False))
+    ks[-1] = n_out - 1
+    ks[0] = 0
+    xh = _host(x)
+    amh = _host(am)
+    for k in ks:
+        seg = xh[k * D: k * D + T]
+        y64, bound = orc.fir_f64(taps, seg, D, 1)
+        assert abs(amh[k] - abs(y64[0])) <= FIR_TOL * bound[0], int(k)
+    del torch
+
+
+def test_graph_capture_replay(ops, orc):
+    """The steady-state chain step is capturable into a HIP graph and replays correctly."""
+    import torch
+    T, D, n_out = 127, 1, 1 << 16
+    n_in = n_out - 1 + T
+    taps = _dev(orc.lowpass_taps(T, 0.1))
+    iq = ops.synth_iq_int8(7, 20e6, 1e3, 1.5e6, 0, n_in)
+    out = torch.empty(n_out, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.fir(taps, iq, D, n_out, out=out, int8_iq=True, am=True)  # warm-up (sets LDS attrs)
+    torch.cuda.current_stream().wait_stream(s)
+    ref = _host(out).copy()
+    g = torch.cuda.CUDAGraph()
+    out.zero_()
+    with torch.cuda.graph(g):
+        ops.fir(taps, iq, D, n_out, out=out, int8_iq=True, am=True)
+    g.replay()
+    assert _host(out).tobytes() == ref.tobytes()
+    ops.synth_iq_int8(8, 20e6, 1e3, 1.5e6, 0, n_in, out=iq)  # new data, same buffers
+    g.replay()
+    x = orc.int8_to_float(_host(iq)).view(np.complex64)
+    y64, bound = orc.fir_f64(_host(taps), x, D, n_out)
+    assert np.all(np.abs(_host(out) - np.abs(y64)) <= FIR_TOL * bound)
