@@ -1,0 +1,204 @@
+// Flat C view of the gpusdrpipeline object model (include/gsdr/gpusdr_flat.h).
+#include <gsdr/gpusdr_flat.h>
+
+#include <gpusdrpipeline/Factories.h>
+#include <gpusdrpipeline/abi/errors.h>
+
+#include <vector>
+
+namespace {
+
+IFactories* factories() {
+  static IFactories* f = getFactoriesSingleton().value;
+  return f;
+}
+
+template <typename T>
+T* as(gspHandle h) {
+  return h == nullptr ? nullptr : dynamic_cast<T*>(static_cast<IRef*>(h));
+}
+
+// Hand a (possibly floating) object to the caller with one reference.
+template <typename T>
+uint32_t give(RefResult<T>&& r, gspHandle* out) {
+  if (out == nullptr) {
+    if (r.value != nullptr && r.status == Status_Success) r.value->unref();
+    return Status_InvalidArgument;
+  }
+  *out = nullptr;
+  if (r.status != Status_Success) {
+    if (r.value != nullptr) r.value->unref();
+    return r.status;
+  }
+  IRef* ref = static_cast<IRef*>(r.value);
+  ref->ref();
+  *out = ref;
+  return Status_Success;
+}
+
+uint32_t push(gspHandle node, size_t port, const void* src, size_t bytes, gspHandle queue, hipMemcpyKind kind) {
+  Sink* sink = as<Sink>(node);
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (sink == nullptr || q == nullptr || (src == nullptr && bytes != 0)) return Status_InvalidArgument;
+  Ref<IBuffer> b;
+  UNWRAP_OR_FWD_STATUS(b, sink->requestBuffer(port, bytes));
+  if (bytes != 0) {
+    HIP_DEV_PUSH_POP_OR_RET_STATUS(q->cudaDevice());
+    const hipError_t e = hipMemcpyAsync(b.get()->writePtr(), src, bytes, kind, q->cudaStream());
+    if (e != hipSuccess) {
+      (void)sink->commitBuffer(port, 0);  // cancel the checkout
+      return hipErrorToStatus(e);
+    }
+  }
+  return sink->commitBuffer(port, bytes);
+}
+
+}  // namespace
+
+extern "C" {
+
+void gspRelease(gspHandle h) {
+  if (h != nullptr) static_cast<IRef*>(h)->unref();
+}
+
+uint32_t gspQueueCreate(int32_t device, gspHandle* queueOut) {
+  return give(factories()->getCudaCommandQueueFactory()->create(device), queueOut);
+}
+
+hipStream_t gspQueueStream(gspHandle queue) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  return q == nullptr ? nullptr : q->cudaStream();
+}
+
+uint32_t gspQueueSync(gspHandle queue) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (q == nullptr) return Status_InvalidArgument;
+  HIP_DEV_PUSH_POP_OR_RET_STATUS(q->cudaDevice());
+  SAFE_HIP_OR_RET_STATUS(hipStreamSynchronize(q->cudaStream()));
+  return Status_Success;
+}
+
+uint32_t gspFirCreate(uint32_t tapType, uint32_t elementType, size_t decimation, const float* taps, size_t tapCount,
+                      gspHandle queue, gspHandle* filterOut) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (q == nullptr) return Status_InvalidArgument;
+  return give(factories()->getFirFactory()->createFir(tapType, elementType, decimation, taps, tapCount, q), filterOut);
+}
+
+uint32_t gspQuadAmDemodCreate(gspHandle queue, gspHandle* filterOut) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (q == nullptr) return Status_InvalidArgument;
+  return give(factories()->getQuadDemodFactory()->createQuadDemod(Modulation_Am, 0.0f, 0.0f, q), filterOut);
+}
+
+uint32_t gspInt8ToFloatCreate(gspHandle queue, gspHandle* filterOut) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (q == nullptr) return Status_InvalidArgument;
+  return give(factories()->getInt8ToFloatFactory()->createFilter(q), filterOut);
+}
+
+uint32_t gspCosineSourceCreate(uint32_t sampleType, float sampleRate, float frequency, gspHandle queue,
+                               gspHandle* sourceOut) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (q == nullptr) return Status_InvalidArgument;
+  return give(factories()->getCosineSourceFactory()->createCosineSource(sampleType, sampleRate, frequency, q),
+              sourceOut);
+}
+
+uint32_t gspNamedQueueCreate(const char* queueId, const char* json) {
+  return factories()->getCommandQueueFactory()->create(queueId, json);
+}
+
+uint32_t gspNodeCreate(const char* name, const char* json, gspHandle* nodeOut) {
+  if (!hasNodeFactory("Fir")) {
+    const Status st = registerDefaultNodeFactories();
+    if (st != Status_Success) return st;
+  }
+  return give(createNode(name, json), nodeOut);
+}
+
+uint32_t gspSinkPushHost(gspHandle node, size_t port, const void* host, size_t bytes, gspHandle queue) {
+  return push(node, port, host, bytes, queue, hipMemcpyHostToDevice);
+}
+
+uint32_t gspSinkPushDevice(gspHandle node, size_t port, const void* device, size_t bytes, gspHandle queue) {
+  return push(node, port, device, bytes, queue, hipMemcpyDeviceToDevice);
+}
+
+uint32_t gspSinkPreferredInputSize(gspHandle node, size_t port, size_t* bytesOut) {
+  Sink* s = as<Sink>(node);
+  if (s == nullptr || bytesOut == nullptr) return Status_InvalidArgument;
+  *bytesOut = s->preferredInputBufferSize(port);
+  return Status_Success;
+}
+
+uint32_t gspSourceOutputSize(gspHandle node, size_t port, size_t* bytesOut, size_t* alignmentOut) {
+  Source* s = as<Source>(node);
+  if (s == nullptr) return Status_InvalidArgument;
+  if (bytesOut) *bytesOut = s->getOutputDataSize(port);
+  if (alignmentOut) *alignmentOut = s->getOutputSizeAlignment(port);
+  return Status_Success;
+}
+
+uint32_t gspSourceRead(gspHandle node, gspHandle* buffers, size_t bufferCount) {
+  Source* s = as<Source>(node);
+  if (s == nullptr || (buffers == nullptr && bufferCount != 0)) return Status_InvalidArgument;
+  try {
+    std::vector<IBuffer*> bufs(bufferCount);
+    for (size_t i = 0; i < bufferCount; ++i) {
+      bufs[i] = as<IBuffer>(buffers[i]);
+      if (bufs[i] == nullptr) return Status_InvalidArgument;
+    }
+    return s->readOutput(bufs.data(), bufferCount);
+  }
+  IF_CATCH_RETURN_STATUS;
+}
+
+uint32_t gspBufferCreate(gspHandle queue, size_t bytes, gspHandle* bufferOut) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (q == nullptr) return Status_InvalidArgument;
+  Ref<IAllocator> alloc;
+  Ref<IBufferFactory> bf;
+  UNWRAP_OR_FWD_STATUS(alloc, factories()->getCudaAllocatorFactory()->createCudaAllocator(q, 32, false));
+  UNWRAP_OR_FWD_STATUS(bf, factories()->createBufferFactory(alloc.get().get()));
+  return give(bf.get()->createBuffer(bytes), bufferOut);
+}
+
+uint32_t gspBufferSlice(gspHandle buffer, size_t start, size_t end, gspHandle* sliceOut) {
+  IBuffer* b = as<IBuffer>(buffer);
+  if (b == nullptr) return Status_InvalidArgument;
+  return give(factories()->getBufferSliceFactory()->slice(b, start, end), sliceOut);
+}
+
+uint32_t gspBufferRange(gspHandle buffer, size_t* offset, size_t* endOffset, size_t* capacity) {
+  IBuffer* b = as<IBuffer>(buffer);
+  if (b == nullptr) return Status_InvalidArgument;
+  if (offset) *offset = b->range()->offset();
+  if (endOffset) *endOffset = b->range()->endOffset();
+  if (capacity) *capacity = b->range()->capacity();
+  return Status_Success;
+}
+
+uint32_t gspBufferSetRange(gspHandle buffer, size_t offset, size_t endOffset) {
+  IBuffer* b = as<IBuffer>(buffer);
+  if (b == nullptr) return Status_InvalidArgument;
+  return b->range()->setUsedRange(offset, endOffset);
+}
+
+void* gspBufferBase(gspHandle buffer) {
+  IBuffer* b = as<IBuffer>(buffer);
+  return b == nullptr ? nullptr : b->base();
+}
+
+uint32_t gspBufferToHost(gspHandle buffer, void* host, size_t bytes, gspHandle queue) {
+  IBuffer* b = as<IBuffer>(buffer);
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (b == nullptr || q == nullptr || (host == nullptr && bytes != 0)) return Status_InvalidArgument;
+  const size_t n = bytes < b->range()->used() ? bytes : b->range()->used();
+  HIP_DEV_PUSH_POP_OR_RET_STATUS(q->cudaDevice());
+  if (n != 0) SAFE_HIP_OR_RET_STATUS(hipMemcpyAsync(host, b->readPtr(), n, hipMemcpyDeviceToHost, q->cudaStream()));
+  SAFE_HIP_OR_RET_STATUS(hipStreamSynchronize(q->cudaStream()));
+  return Status_Success;
+}
+
+}  // extern "C"

@@ -1,0 +1,117 @@
+// Hot-path filters over the gsdr gfx950 kernels (reference src/filters): Fir (Fir.cpp:32-311),
+// QuadAmDemod (QuadAmDemod.cpp:28-109), Int8ToFloat (Int8ToFloat.cpp:30-102), CosineSource /
+// ComplexCosineSource (CosineSource.cpp:28-88), and the H2D/D2H staging filter
+// (CudaMemcpyFilter.cpp:28-104). Each readOutput() enqueues exactly one kernel (or copy) on the
+// queue's stream and returns without synchronising, as in the reference.
+#pragma once
+
+#include <gpusdrpipeline/Factories.h>
+#include <gpusdrpipeline/abi/base_filters.h>
+#include <gpusdrpipeline/abi/errors.h>
+
+namespace gsdr_rt {
+
+// Bytes per element of each SampleType on a filter's *input* side. Int8Complex is one I/Q
+// pair (2 bytes); the reference's 1-byte size (Fir.cpp:34-45) never produced output.
+size_t inputElementSize(SampleType t) noexcept;
+
+class Fir final : public BaseFilter {
+ public:
+  static Result<Filter> create(SampleType tapType, SampleType elementType, size_t decimation, const float* taps,
+                               size_t tapCount, ICudaCommandQueue* queue, IFactories* factories) noexcept;
+
+  size_t getOutputDataSize(size_t port) noexcept final;
+  size_t getOutputSizeAlignment(size_t port) noexcept final;
+  Status readOutput(IBuffer** portOutputBuffers, size_t numPorts) noexcept final;
+  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+
+  size_t decimation() const noexcept { return mDecimation; }
+  size_t tapCount() const noexcept { return mTapCount; }
+
+ private:
+  Fir(SampleType tapType, SampleType elementType, size_t decimation, ICudaCommandQueue* queue, IAllocator* allocator,
+      IBufferCopier* h2d, IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices, IMemSet* memSet,
+      std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept;
+  Status setTaps(const float* taps, size_t tapCount) noexcept;
+  size_t availableInputs() const noexcept;
+  size_t availableOutputs() const noexcept;
+
+  const SampleType mTapType;
+  const SampleType mElementType;
+  ConstRef<IAllocator> mAllocator;
+  ConstRef<IBufferCopier> mH2D;
+  const size_t mDecimation;
+  Ref<IMemory> mTaps;
+  size_t mTapCount = 0;
+  ConstRef<ICudaCommandQueue> mQueue;
+  const size_t mInElem;
+  const size_t mOutElem;
+
+  REF_COUNTED(Fir);
+};
+
+class QuadAmDemod final : public BaseFilter {
+ public:
+  static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
+  size_t getOutputDataSize(size_t port) noexcept final;
+  size_t getOutputSizeAlignment(size_t port) noexcept final;
+  Status readOutput(IBuffer** portOutputBuffers, size_t numPorts) noexcept final;
+  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+
+ private:
+  QuadAmDemod(ICudaCommandQueue* queue, IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
+              IMemSet* memSet, std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept;
+  ConstRef<ICudaCommandQueue> mQueue;
+  REF_COUNTED(QuadAmDemod);
+};
+
+class Int8ToFloat final : public BaseFilter {
+ public:
+  static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
+  size_t getOutputDataSize(size_t port) noexcept final;
+  size_t getOutputSizeAlignment(size_t port) noexcept final;
+  Status readOutput(IBuffer** portOutputBuffers, size_t numPorts) noexcept final;
+  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+
+ private:
+  Int8ToFloat(ICudaCommandQueue* queue, IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
+              IMemSet* memSet, std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept;
+  ConstRef<ICudaCommandQueue> mQueue;
+  REF_COUNTED(Int8ToFloat);
+};
+
+// Infinite phase-continuous tone (cos for Float, exp(j phi) for FloatComplex).
+class CosineSource final : public BaseSource {
+ public:
+  static Result<Source> create(bool complexOutput, float sampleRate, float frequency, ICudaCommandQueue* queue,
+                               IFactories* factories) noexcept;
+  size_t getOutputDataSize(size_t port) noexcept final;
+  size_t getOutputSizeAlignment(size_t port) noexcept final;
+  Status readOutput(IBuffer** portOutputBuffers, size_t numPorts) noexcept final;
+
+ private:
+  CosineSource(bool complexOutput, float sampleRate, float frequency, ICudaCommandQueue* queue,
+               std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept;
+  const bool mComplex;
+  const float mRadiansPerSample;
+  ConstRef<ICudaCommandQueue> mQueue;
+  float mPhi = 0.0f;
+  REF_COUNTED(CosineSource);
+};
+
+class HipMemcpyFilter final : public BaseFilter {
+ public:
+  static Result<Filter> create(hipMemcpyKind kind, ICudaCommandQueue* queue, IFactories* factories) noexcept;
+  size_t getOutputDataSize(size_t port) noexcept final;
+  size_t getOutputSizeAlignment(size_t port) noexcept final;
+  Status readOutput(IBuffer** portOutputBuffers, size_t numPorts) noexcept final;
+  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+
+ private:
+  HipMemcpyFilter(IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices, IMemSet* memSet,
+                  IBufferCopier* copier, std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept;
+  ConstRef<IBufferCopier> mCopier;
+  REF_COUNTED(HipMemcpyFilter);
+};
+
+}  // namespace gsdr_rt

@@ -1,0 +1,204 @@
+"""Python handles over the gpusdrpipeline filter graph (flat C API, include/gsdr/gpusdr_flat.h).
+
+Mirrors the reference's node interface (src/filters/Fir.cpp etc.): nodes are created through
+the factories, fed through Sink.requestBuffer/commitBuffer (``push``) and drained through
+Source.readOutput into device buffers (``read``). Every call lands in libgpusdrpipeline.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._native import lib
+
+SAMPLE_FLOAT_COMPLEX, SAMPLE_FLOAT, SAMPLE_INT8_COMPLEX = 0, 1, 2
+STATUS_NAMES = ["Success", "UnknownError", "OutOfMemory", "RuntimeError", "InvalidArgument", "InvalidState",
+                "OutOfRange", "TimedOut", "NotFound", "ParseError"]
+
+
+class GraphError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        name = STATUS_NAMES[status] if status < len(STATUS_NAMES) else str(status)
+        super().__init__(f"{what}: Status_{name}")
+        self.status = status
+
+
+_declared = False
+
+
+def _L():
+    global _declared
+    L = lib()
+    if not _declared:
+        h, sz, u32, vp = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p
+        ph = ctypes.POINTER(ctypes.c_void_p)
+        psz = ctypes.POINTER(ctypes.c_size_t)
+        sigs = {
+            "gspRelease": ([h], None),
+            "gspQueueCreate": ([ctypes.c_int32, ph], u32),
+            "gspQueueStream": ([h], vp),
+            "gspQueueSync": ([h], u32),
+            "gspFirCreate": ([u32, u32, sz, vp, sz, h, ph], u32),
+            "gspQuadAmDemodCreate": ([h, ph], u32),
+            "gspInt8ToFloatCreate": ([h, ph], u32),
+            "gspCosineSourceCreate": ([u32, ctypes.c_float, ctypes.c_float, h, ph], u32),
+            "gspNamedQueueCreate": ([ctypes.c_char_p, ctypes.c_char_p], u32),
+            "gspNodeCreate": ([ctypes.c_char_p, ctypes.c_char_p, ph], u32),
+            "gspSinkPushHost": ([h, sz, vp, sz, h], u32),
+            "gspSinkPushDevice": ([h, sz, vp, sz, h], u32),
+            "gspSinkPreferredInputSize": ([h, sz, psz], u32),
+            "gspSourceOutputSize": ([h, sz, psz, psz], u32),
+            "gspSourceRead": ([h, ph, sz], u32),
+            "gspBufferCreate": ([h, sz, ph], u32),
+            "gspBufferSlice": ([h, sz, sz, ph], u32),
+            "gspBufferRange": ([h, psz, psz, psz], u32),
+            "gspBufferSetRange": ([h, sz, sz], u32),
+            "gspBufferBase": ([h], vp),
+            "gspBufferToHost": ([h, vp, sz, h], u32),
+        }
+        for name, (args, res) in sigs.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _declared = True
+    return L
+
+
+def _check(status, what):
+    if status != 0:
+        raise GraphError(status, what)
+
+
+class _Handle:
+    def __init__(self, ptr):
+        self._h = ctypes.c_void_p(ptr)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def release(self):
+        if self._h:
+            _L().gspRelease(self._h)
+            self._h = ctypes.c_void_p(None)
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:
+            pass
+
+
+def _create(fn, *args, what=""):
+    out = ctypes.c_void_p()
+    _check(fn(*args, ctypes.byref(out)), what)
+    return out.value
+
+
+class Queue(_Handle):
+    """ICudaCommandQueue: one HIP device + one non-blocking stream."""
+
+    def __init__(self, device: int = 0):
+        super().__init__(_create(_L().gspQueueCreate, device, what="gspQueueCreate"))
+
+    @property
+    def stream(self) -> int:
+        return _L().gspQueueStream(self._h)
+
+    def sync(self):
+        _check(_L().gspQueueSync(self._h), "gspQueueSync")
+
+
+class Buffer(_Handle):
+    """IBuffer over device memory (or a slice of one)."""
+
+    def __init__(self, ptr, queue: Queue, parent=None):
+        super().__init__(ptr)
+        self.queue = queue
+        self._parent = parent
+
+    @classmethod
+    def create(cls, queue: Queue, nbytes: int) -> "Buffer":
+        return cls(_create(_L().gspBufferCreate, queue.handle, nbytes, what="gspBufferCreate"), queue)
+
+    def slice(self, start: int, end: int) -> "Buffer":
+        return Buffer(_create(_L().gspBufferSlice, self._h, start, end, what="gspBufferSlice"), self.queue, self)
+
+    def range(self):
+        o, e, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        _check(_L().gspBufferRange(self._h, ctypes.byref(o), ctypes.byref(e), ctypes.byref(c)), "gspBufferRange")
+        return o.value, e.value, c.value
+
+    def used(self) -> int:
+        o, e, _ = self.range()
+        return e - o
+
+    def set_range(self, offset: int, end: int):
+        _check(_L().gspBufferSetRange(self._h, offset, end), "gspBufferSetRange")
+
+    def clear(self):
+        self.set_range(0, 0)
+
+    def to_host(self, dtype) -> np.ndarray:
+        n = self.used()
+        out = np.empty(n, dtype=np.uint8)
+        _check(_L().gspBufferToHost(self._h, out.ctypes.data, n, self.queue.handle), "gspBufferToHost")
+        return out.view(dtype)
+
+
+class Node(_Handle):
+    """A Filter / Source / Sink of the reference object model."""
+
+    def __init__(self, ptr, queue: Queue | None):
+        super().__init__(ptr)
+        self.queue = queue
+
+    # -- constructors mirroring the reference factories --
+    @classmethod
+    def fir(cls, queue: Queue, taps: np.ndarray, decimation: int = 1, element_type: int = SAMPLE_FLOAT_COMPLEX):
+        taps_c = np.iscomplexobj(taps)
+        t = np.ascontiguousarray(taps, dtype=np.complex64 if taps_c else np.float32)
+        tap_type = SAMPLE_FLOAT_COMPLEX if taps_c else SAMPLE_FLOAT
+        return cls(_create(_L().gspFirCreate, tap_type, element_type, decimation, t.ctypes.data, len(t), queue.handle,
+                           what="gspFirCreate"), queue)
+
+    @classmethod
+    def quad_am_demod(cls, queue: Queue):
+        return cls(_create(_L().gspQuadAmDemodCreate, queue.handle, what="gspQuadAmDemodCreate"), queue)
+
+    @classmethod
+    def int8_to_float(cls, queue: Queue):
+        return cls(_create(_L().gspInt8ToFloatCreate, queue.handle, what="gspInt8ToFloatCreate"), queue)
+
+    @classmethod
+    def cosine(cls, queue: Queue, sample_type: int, sample_rate: float, frequency: float):
+        return cls(_create(_L().gspCosineSourceCreate, sample_type, sample_rate, frequency, queue.handle,
+                           what="gspCosineSourceCreate"), queue)
+
+    @classmethod
+    def from_json(cls, name: str, params: str, queue: Queue | None = None):
+        return cls(_create(_L().gspNodeCreate, name.encode(), params.encode(), what=f"createNode({name})"), queue)
+
+    # -- Sink --
+    def push(self, data: np.ndarray, port: int = 0):
+        a = np.ascontiguousarray(data)
+        _check(_L().gspSinkPushHost(self._h, port, a.ctypes.data, a.nbytes, self.queue.handle), "push")
+
+    def push_device(self, ptr: int, nbytes: int, port: int = 0):
+        _check(_L().gspSinkPushDevice(self._h, port, ptr, nbytes, self.queue.handle), "push_device")
+
+    def preferred_input_size(self, port: int = 0) -> int:
+        n = ctypes.c_size_t()
+        _check(_L().gspSinkPreferredInputSize(self._h, port, ctypes.byref(n)), "preferredInputBufferSize")
+        return n.value
+
+    # -- Source --
+    def output_size(self, port: int = 0):
+        n, a = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(_L().gspSourceOutputSize(self._h, port, ctypes.byref(n), ctypes.byref(a)), "getOutputDataSize")
+        return n.value, a.value
+
+    def read(self, buffers):
+        arr = (ctypes.c_void_p * len(buffers))(*[b.handle.value for b in buffers])
+        _check(_L().gspSourceRead(self._h, arr, len(buffers)), "readOutput")

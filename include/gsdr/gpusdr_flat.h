@@ -1,0 +1,79 @@
+/*
+ * gpusdr_flat.h - a flat C view of the gpusdrpipeline object model for foreign-function
+ * callers (Python ctypes in tests/ and bench.py; any cgo / JNI / N-API binding).
+ *
+ * Every handle is an IRef-derived object holding ONE reference owned by the caller; release it
+ * with gspRelease(). Functions return a Status (0 = Status_Success, include/gpusdrpipeline
+ * abi/core.h) and never throw. Device work is enqueued on the queue's HIP stream; only
+ * gspQueueSync() and gspBufferToHost() block.
+ *
+ * Reference interfaces each call forwards to:
+ *   gspQueueCreate           ICudaCommandQueueFactory::create   (ICudaCommandQueueFactory.h:11-16)
+ *   gspFirCreate             IFirFactory::createFir             (FilterFactories.h:101-112)
+ *   gspQuadAmDemodCreate     IQuadDemodFactory::createQuadDemod (FilterFactories.h:146-157)
+ *   gspInt8ToFloatCreate     ICudaFilterFactory::createFilter   (FilterFactories.h:125-130)
+ *   gspCosineSourceCreate    ICosineSourceFactory::createCosineSource
+ *   gspNodeCreate            createNode (registry, FilterFactories.h:36)
+ *   gspSinkPushHost          Sink::requestBuffer + H2D copy + Sink::commitBuffer (Filter.h:40-66)
+ *   gspSourceOutputSize      Source::getOutputDataSize / getOutputSizeAlignment (Filter.h:70-87)
+ *   gspSourceRead            Source::readOutput (Filter.h:111-121)
+ *   gspBuffer*               IBufferFactory / IBufferSliceFactory / IBufferRange
+ */
+#ifndef GSDR_GPUSDR_FLAT_H
+#define GSDR_GPUSDR_FLAT_H
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define GSP_API __attribute__((visibility("default")))
+#else
+#define GSP_API
+#endif
+
+typedef void* gspHandle; /* an IRef-derived object; one caller-owned reference */
+
+GSP_API void gspRelease(gspHandle h);
+
+GSP_API uint32_t gspQueueCreate(int32_t device, gspHandle* queueOut);
+GSP_API hipStream_t gspQueueStream(gspHandle queue);
+GSP_API uint32_t gspQueueSync(gspHandle queue);
+
+/* sampleType values: 0 FloatComplex, 1 Float, 2 Int8Complex (SampleType.h:20-25). taps is host memory. */
+GSP_API uint32_t gspFirCreate(uint32_t tapType, uint32_t elementType, size_t decimation, const float* taps,
+                              size_t tapCount, gspHandle queue, gspHandle* filterOut);
+GSP_API uint32_t gspQuadAmDemodCreate(gspHandle queue, gspHandle* filterOut);
+GSP_API uint32_t gspInt8ToFloatCreate(gspHandle queue, gspHandle* filterOut);
+GSP_API uint32_t gspCosineSourceCreate(uint32_t sampleType, float sampleRate, float frequency, gspHandle queue,
+                                       gspHandle* sourceOut);
+GSP_API uint32_t gspNamedQueueCreate(const char* queueId, const char* json);
+GSP_API uint32_t gspNodeCreate(const char* name, const char* json, gspHandle* nodeOut);
+
+/* Sink side of a filter node: append host bytes to input port `port`. */
+GSP_API uint32_t gspSinkPushHost(gspHandle node, size_t port, const void* host, size_t bytes, gspHandle queue);
+/* Sink side: append bytes already on the device (D2D copy on the queue). */
+GSP_API uint32_t gspSinkPushDevice(gspHandle node, size_t port, const void* device, size_t bytes, gspHandle queue);
+GSP_API uint32_t gspSinkPreferredInputSize(gspHandle node, size_t port, size_t* bytesOut);
+
+GSP_API uint32_t gspSourceOutputSize(gspHandle node, size_t port, size_t* bytesOut, size_t* alignmentOut);
+GSP_API uint32_t gspSourceRead(gspHandle node, gspHandle* buffers, size_t bufferCount);
+
+/* Device buffers (32-byte aligned device memory from the queue's stream-ordered pool). */
+GSP_API uint32_t gspBufferCreate(gspHandle queue, size_t bytes, gspHandle* bufferOut);
+GSP_API uint32_t gspBufferSlice(gspHandle buffer, size_t start, size_t end, gspHandle* sliceOut);
+GSP_API uint32_t gspBufferRange(gspHandle buffer, size_t* offset, size_t* endOffset, size_t* capacity);
+GSP_API uint32_t gspBufferSetRange(gspHandle buffer, size_t offset, size_t endOffset);
+GSP_API void* gspBufferBase(gspHandle buffer);
+/* Copies the buffer's used bytes (at most `bytes`) to host and synchronises the queue. */
+GSP_API uint32_t gspBufferToHost(gspHandle buffer, void* host, size_t bytes, gspHandle queue);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSDR_GPUSDR_FLAT_H */

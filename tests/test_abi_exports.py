@@ -8,7 +8,8 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "cuda-sdr_amd", "lib", "libgpusdrpipeline.so")
-EXPORT_RE = re.compile(r"^\s*(?:GSDR_API|GSDR_CONV_API|GS_EXPORT)\b[^(]*?\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", re.M)
+EXPORT_RE = re.compile(r"^\s*(?:GSDR_API|GSDR_CONV_API|GSP_API|GS_EXPORT)\b[^(]*?\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", re.M)
+NOISE_RE = re.compile(r"GS_FMT_ATTR\([^)]*\)|\[\[[^\]]*\]\]")
 
 
 def declared_symbols():
@@ -17,7 +18,7 @@ def declared_symbols():
         for f in files:
             if f.endswith(".h"):
                 with open(os.path.join(root, f)) as fh:
-                    names.update(EXPORT_RE.findall(fh.read()))
+                    names.update(EXPORT_RE.findall(NOISE_RE.sub("", fh.read())))
     return names
 
 

@@ -1,0 +1,137 @@
+"""The filter-graph boundary (gpusdrpipeline C++ ABI) on the GPU.
+
+* the reference's own FIR / cosine known-answer tests, compiled as C++ against
+  include/gpusdrpipeline (tests/cpp/abi_kats.cpp), run as a binary;
+* the streaming contract replayed against the oracle's restatement
+  (oracle.FirStreamModel: BaseSink.cpp:61-170 window, Fir.cpp:141-279 count/consume,
+  partial reads of FirTests.cpp:96-221) under random chunking and random output capacities.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIR_TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def graph():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from gpusdr import graph as g
+    return g
+
+
+@pytest.fixture(scope="module")
+def queue(graph):
+    return graph.Queue(0)
+
+
+def test_cpp_abi_kats():
+    exe = os.path.join(REPO, "tests", "cpp", "_build", "abi_kats")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "cpp")], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ALL PASS" in r.stdout, r.stdout + r.stderr
+
+
+def _drain(graph, queue, node, capacity, dtype):
+    buf = graph.Buffer.create(queue, capacity)
+    sl = buf.slice(0, capacity)
+    sl.clear()
+    node.read([sl])
+    return sl.to_host(dtype)
+
+
+@pytest.mark.parametrize("T,D,elem", [(2, 2, "c"), (127, 1, "c"), (63, 3, "f"), (1023, 10, "c"), (31, 4, "cc"),
+                                      (64, 5, "cf"), (127, 1, "i8")])
+def test_fir_streaming_matches_model(graph, queue, orc, T, D, elem):
+    rng = np.random.default_rng(T * 10 + D)
+    taps = orc.lowpass_taps(T, 0.4 / D) if T > 2 else np.array([0.5, 1.0], np.float32)
+    if elem in ("cc", "cf"):
+        taps = (taps * np.exp(0.2j * np.arange(T))).astype(np.complex64)
+    et = {"c": graph.SAMPLE_FLOAT_COMPLEX, "cc": graph.SAMPLE_FLOAT_COMPLEX, "f": graph.SAMPLE_FLOAT,
+          "cf": graph.SAMPLE_FLOAT, "i8": graph.SAMPLE_INT8_COMPLEX}[elem]
+    node = graph.Node.fir(queue, taps, D, et)
+    model = orc.FirStreamModel(taps, D)
+    out_elem = 4 if (elem == "f") else 8
+    out_dtype = np.float32 if elem == "f" else np.complex64
+    total_out = 0
+    for step in range(25):
+        n = int(rng.integers(0, 3 * T + 50))
+        if elem in ("c", "cc"):
+            x = (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+            node.push(x)
+            model.push(x)
+        elif elem in ("f", "cf"):
+            x = rng.standard_normal(n).astype(np.float32)
+            node.push(x)
+            model.push(x)
+        else:
+            iq = rng.integers(-128, 128, size=2 * n).astype(np.int8)
+            node.push(iq)
+            model.push(orc.int8_to_float(iq).view(np.complex64))
+        size, align = node.output_size()
+        assert size == model.output_count() * out_elem
+        assert align == 32 * out_elem
+        cap = int(rng.integers(1, 40)) * out_elem
+        y = _drain(graph, queue, node, cap, out_dtype)
+        y64, bound = model.read(cap // out_elem)
+        assert len(y) == len(y64)
+        total_out += len(y)
+        if len(y):
+            assert np.all(np.abs(y.astype(np.complex128) - y64) <= FIR_TOL * bound + 1e-30), step
+    assert total_out > 0
+
+
+def test_elementwise_filters_bit_exact(graph, queue, orc):
+    rng = np.random.default_rng(9)
+    conv = graph.Node.int8_to_float(queue)
+    am = graph.Node.quad_am_demod(queue)
+    for _ in range(10):
+        iq = rng.integers(-128, 128, size=int(rng.integers(1, 5000))).astype(np.int8)
+        conv.push(iq)
+        got = _drain(graph, queue, conv, 4 * len(iq) + 64, np.float32)
+        assert got.tobytes() == orc.int8_to_float(iq).tobytes()
+        z = (rng.standard_normal(len(iq)) * 5 + 1j * rng.standard_normal(len(iq))).astype(np.complex64)
+        am.push(z)
+        got = _drain(graph, queue, am, 4 * len(z), np.float32)
+        assert got.tobytes() == orc.quad_am_demod(z).tobytes()
+
+
+def test_cosine_source_phase_continuity(graph, queue, orc):
+    src = graph.Node.cosine(queue, graph.SAMPLE_FLOAT_COMPLEX, 48000.0, 1234.5)
+    assert src.output_size()[0] == 2 ** 64 - 1  # infinite source (CosineSource.cpp:59)
+    delta = np.float32(2.0 * np.pi * 1234.5 / 48000.0)
+    phi = np.float32(0.0)
+    for n in (100, 37, 4096):
+        z = _drain(graph, queue, src, 8 * n, np.complex64)
+        assert len(z) == n
+        phi_end = np.float32(phi + np.float32(n) * delta)
+        ref = orc.cosine_c(float(phi), float(phi_end), n)
+        assert np.max(np.abs(z - ref)) < 2e-5
+        phi = np.float32(np.fmod(phi_end, np.float32(2.0 * np.pi)))
+
+
+def test_json_nodes_and_out_of_scope(graph, queue):
+    from gpusdr._native import lib
+    import ctypes
+    assert graph._L().gspNamedQueueCreate(b"q0", b'{"queueType": "hip", "cudaDevice": 0}') == 0
+    fir = graph.Node.from_json("Fir", '{"commandQueue": "q0", "taps": [0.5, 1.0], "tapType": "Float", '
+                                      '"elementType": "FloatComplex", "decimation": 2}', queue)
+    fir.push(np.array([0.1 + 0.2j, 0.3 + 0.4j, 0.5 + 0.6j, 0.7 + 0.8j, 0.9 + 0.9j], np.complex64))
+    y = _drain(graph, queue, fir, 64, np.complex64)
+    assert np.allclose(y, [0.35 + 0.5j, 0.95 + 1.1j], atol=1e-6)
+    for name in ("MultiplyCCC", "HackRfSource", "AacWriter"):
+        with pytest.raises(graph.GraphError) as e:
+            graph.Node.from_json(name, '{"commandQueue": "q0"}')
+        assert e.value.status == 8  # Status_NotFound
+    with pytest.raises(graph.GraphError) as e:
+        graph.Node.from_json("Fir", "{broken")
+    assert e.value.status == 9  # Status_ParseError
+    del lib, ctypes

@@ -77,9 +77,9 @@ RAGGED = [
 def test_fir_ragged(ops, orc, T, D, n_out, mode):
     rng = np.random.default_rng(T * 131 + D * 7 + n_out)
     n_in = (n_out - 1) * D + T
-    taps = rng.standard_normal(T).astype(np.float32) / np.sqrt(T)
+    taps = (rng.standard_normal(T) / np.sqrt(T)).astype(np.float32)
     if mode[0] == "C":
-        taps = (taps + 1j * rng.standard_normal(T).astype(np.float32) / np.sqrt(T)).astype(np.complex64)
+        taps = (taps + 1j * rng.standard_normal(T) / np.sqrt(T)).astype(np.complex64)
     if mode[1] == "C":
         x = (rng.standard_normal(n_in) + 1j * rng.standard_normal(n_in)).astype(np.complex64)
     else:
