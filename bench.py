@@ -15,7 +15,7 @@ halo <- g-1, RCCL over xGMI), overlapped with the bulk kernel that needs no halo
 head kernel finishes the first T-1 outputs once the halo has landed.
 
 Other workloads (--workload): c3 (cf32 2^28, 1023 taps, D=10, FIR->AM), c4 (cf32, 1023 taps,
-D=1, FIR->AM), c5 (int8 -> 1023-tap FIR D=10 -> AM -> 255-tap audio FIR D=20).
+D=1, FIR->AM).
 
 Output: one JSON line on rank 0 (contract in the task statement) with `roofline` for the
 dominant kernel (HIP events on its stream) and `cpu_baseline` (oracle port, rank 0, N=1).
@@ -47,8 +47,6 @@ WORKLOADS = {
            "c64", 1 << 28, 1023, 10, 0.04, "blackman", 200e6),
     "c4": ("C4: cf32 stream, 1023-tap FC FIR, D=1 -> QuadAmDemod, 2^26 samples per GPU step",
            "c64", 1 << 26, 1023, 1, 0.04, "blackman", 1e9),
-    "c5": ("C5: int8 IQ @1 Gsps -> cf32 -> 1023-tap FIR D=10 -> AM -> 255-tap audio FIR D=20, 2^28 per GPU step",
-           "i8", 1 << 28, 1023, 10, 0.04, "blackman", 1e9),
 }
 
 
@@ -78,93 +76,53 @@ def dist_setup(n_gpus):
 
 
 class ShardedChain:
-    """Per-rank state of one time-sharded FIR chain step (see module docstring)."""
+    """Per-rank state of one time-sharded FIR -> AM step (gpusdr/shard.py protocol)."""
 
     def __init__(self, ops, wl, rank, world, device):
+        from gpusdr.shard import HaloRing, ShardGeometry
         desc, kind, L, T, D, cutoff, window, fs = WORKLOADS[wl]
-        self.ops, self.kind, self.L, self.T, self.D, self.fs = ops, kind, L, T, D, fs
-        self.rank, self.world, self.device = rank, world, device
-        self.H = T - 1  # halo samples
+        self.ops, self.kind, self.L, self.T, self.D = ops, kind, L, T, D
+        self.geom = g = ShardGeometry(rank, world, L, T, D)
+        H = g.halo
         self.taps = torch.from_numpy(lowpass(T, cutoff, window)).to(device)
-        self.n_out = L // D
-        assert L % D == 0
-        first = (rank * L)  # stream index of this rank's first sample in step 0
+        w = 2 if kind == "i8" else 1  # tensor elements per sample (int8 I,Q | complex64)
+        dt = torch.int8 if kind == "i8" else torch.complex64
+        self.buf = torch.zeros(w * (H + L), dtype=dt, device=device)  # [halo | segment]
+        self.seg = self.buf[w * H:]
         if kind == "i8":
-            self.buf = torch.empty(2 * (self.H + L), dtype=torch.int8, device=device)
-            self.seg = self.buf[2 * self.H:]
-            ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, first, L, out=self.seg)
-            self.halo = self.buf[: 2 * self.H]
-            self.tail = self.seg[2 * (L - self.H):]
-            self.halo.zero_()
+            ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, g.segment_start(0), L, out=self.seg)
         else:
-            self.buf = torch.empty(self.H + L, dtype=torch.complex64, device=device)
-            self.seg = self.buf[self.H:]
-            ops.synth_wideband_cf32(0xC3, 0.013, 0.31, first, L, out=self.seg)
-            self.halo = self.buf[: self.H]
-            self.tail = self.seg[L - self.H:]
-            self.halo.zero_()
-        self.out = torch.empty(self.n_out, dtype=torch.float32, device=device)
-        # outputs that need no halo: k*D >= H  ->  k >= ceil(H / D)
-        self.k_split = min(self.n_out, (self.H + D - 1) // D)
-        self.audio = None
-        if wl == "c5":
-            self.audio_taps = torch.from_numpy(lowpass(255, 0.4 / 20, "hamming")).to(device)
-            self.audio_D = 20
-            self.audio_H = 254
-            # the audio FIR's own history carry (AM samples of the previous step's tail)
-            self.audio_buf = torch.zeros(self.audio_H + self.n_out, dtype=torch.float32, device=device)
-            self.audio_out = torch.empty(self.n_out // self.audio_D + 1, dtype=torch.float32, device=device)
+            ops.synth_wideband_cf32(0xC3, 0.013, 0.31, g.segment_start(0), L, out=self.seg)
+        incoming = torch.zeros(w * H, dtype=dt, device=device) if (world > 1 and rank == 0) else None
+        self.ring = HaloRing(g, self.buf[: w * H], self.seg[w * (L - H):], incoming)
+        self.bulk_x = self.seg[w * g.bulk_input_offset():]
+        self.out = torch.empty(g.outputs, dtype=torch.float32, device=device)
+        self.ev = None
 
     def _fir(self, x, n_out, out):
-        if n_out <= 0:
-            return
-        self.ops.fir(self.taps, x, self.D, n_out, out=out, am=True, int8_iq=(self.kind == "i8"))
+        if n_out > 0:
+            self.ops.fir(self.taps, x, self.D, n_out, out=out, am=True, int8_iq=(self.kind == "i8"))
 
     def bulk(self):
-        """Outputs [k_split, n_out): inputs entirely inside this rank's segment."""
-        k0 = self.k_split
-        n = self.n_out - k0
-        start = k0 * self.D - self.H  # offset into seg
-        x = self.seg[2 * start:] if self.kind == "i8" else self.seg[start:]
-        self._fir(x, n, self.out[k0:])
+        """Outputs [head, L/D): inputs entirely inside this rank's segment (the timed kernel)."""
+        g = self.geom
+        if self.ev is not None:
+            self.ev[0].record()
+        self._fir(self.bulk_x, g.outputs - g.head_outputs, self.out[g.head_outputs:])
+        if self.ev is not None:
+            self.ev[1].record()
 
     def head(self):
-        """Outputs [0, k_split): need the halo in front of the segment."""
-        x = self.buf
-        self._fir(x, self.k_split, self.out[: self.k_split])
-
-    def exchange_start(self):
-        if self.world == 1:
-            self.halo.copy_(self.tail)  # ring of one: the previous segment is our own
-            return []
-        nxt = (self.rank + 1) % self.world
-        prv = (self.rank - 1) % self.world
-        ops = [dist.P2POp(dist.isend, self.tail, nxt), dist.P2POp(dist.irecv, self.halo, prv)]
-        return dist.batch_isend_irecv(ops)
-
-    def audio_stage(self):
-        if not hasattr(self, "audio_buf"):
-            return
-        # AM output feeds the 255-tap real audio FIR (D=20) with its own (T_a - 1) carry
-        self.audio_buf[self.audio_H:].copy_(self.out)
-        n = (self.audio_H + self.n_out - 255) // self.audio_D + 1
-        self.ops.fir(self.audio_taps, self.audio_buf, self.audio_D, n, out=self.audio_out[:n])
-        self.audio_buf[: self.audio_H].copy_(self.out[self.n_out - self.audio_H:])
+        """Outputs [0, head): read the halo in front of the segment."""
+        self._fir(self.buf, self.geom.head_outputs, self.out[: self.geom.head_outputs])
 
     def step(self, ev=None):
-        reqs = self.exchange_start()
-        if ev is not None:
-            ev[0].record()
-        self.bulk()
-        if ev is not None:
-            ev[1].record()
-        for r in reqs:
-            r.wait()
-        self.head()
-        self.audio_stage()
+        self.ev = ev
+        self.ring.step(self.bulk, self.head)
 
     def bulk_bytes_flops(self):
-        n = self.n_out - self.k_split
+        g = self.geom
+        n = g.outputs - g.head_outputs
         n_in = (n - 1) * self.D + self.T
         in_bytes = n_in * (2 if self.kind == "i8" else 8)
         return in_bytes + n * 4, n * self.T * 4  # algorithmic bytes; direct-form FC flops
@@ -285,7 +243,7 @@ def main():
                 "taps": chain.T,
                 "decimation": chain.D,
                 "input": "int8 IQ" if chain.kind == "i8" else "cf32",
-                "parallelism": f"time-shard x{world} (ring halo of {chain.H} samples over RCCL)"
+                "parallelism": f"time-shard x{world} (ring halo of {chain.geom.halo} samples over RCCL)"
                 if world > 1 else "single GPU (halo = own history carry)",
             },
             "roofline": {

@@ -514,13 +514,22 @@ GS_EXPORT Result<Node> createNode(const char* name, const char* jsonParameters) 
   IF_CATCH_RETURN_RESULT;
 }
 
+// The new node is floating (ref-count 0) and must be handed on floating: holding it in a Ref
+// here would delete it when the Ref goes out of scope. (The reference wraps it in Ref +
+// ConstRef and returns the raw pointer, FilterFactories.cpp:44-65, which leaves the caller a
+// dangling pointer.)
 template <typename T>
 static Result<T> createAs(const char* name, const char* json, T* (Node::*as)() noexcept, const char* what) noexcept {
-  Ref<Node> node;
-  UNWRAP_OR_FWD_RESULT(node, createNode(name, json));
-  T* typed = (node.get().get()->*as)();
+  RefResult<Node> created = createNode(name, json);
+  if (created.status != Status_Success) {
+    if (created.value != nullptr) created.value->unref();
+    return ERR_RESULT(created.status);
+  }
+  Node* node = created.value;
+  T* typed = (node->*as)();
   if (typed == nullptr) {
-    gsloge("[%s] was created, but is not a %s. %s", name, what, kindString(node.get().get()));
+    gsloge("[%s] was created, but is not a %s. %s", name, what, kindString(node));
+    node->unref();  // floating: unref at count 0 deletes
     return ERR_RESULT(Status_InvalidArgument);
   }
   return makeRefResultNonNull<T>(typed);
