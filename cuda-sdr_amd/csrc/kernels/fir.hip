@@ -28,6 +28,8 @@
 #include <gsdr/gsdr.h>
 #include <gsdr/gsdr_amd.h>
 
+#include <atomic>
+
 namespace gsdr_amd {
 
 enum InKind : int { kInF32 = 0, kInCF32 = 1, kInI8IQ = 2 };
@@ -427,6 +429,12 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
   DevicePush push(device);
   if (!push.ok) return hipErrorInvalidDevice;
 
+  // int8 IQ with real taps: the exact int8 MFMA kernel when the shape allows it
+  if constexpr (MODE == kFirFC && INK == kInI8IQ && EPI != kEpiPair) {
+    if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firI8MfmaEligible(tapCount, decimation, in))
+      return launchFirI8Mfma(static_cast<const int8_t*>(in), taps, tapCount, out, nOut, EPI, stream);
+  }
+
   const FirPlanShape s = planFirShape(tapCount, decimation);
   FirArgs a{};
   a.in = in;
@@ -457,9 +465,19 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
 
 }  // namespace gsdr_amd
 
+namespace gsdr_amd {
+namespace {
+std::atomic<uint32_t> gKernelPolicy{0};
+}
+uint32_t kernelPolicy() { return gKernelPolicy.load(std::memory_order_relaxed); }
+}  // namespace gsdr_amd
+
 using namespace gsdr_amd;
 
 extern "C" {
+
+void gsdrAmdSetKernelPolicy(uint32_t flags) { gKernelPolicy.store(flags, std::memory_order_relaxed); }
+uint32_t gsdrAmdGetKernelPolicy(void) { return gKernelPolicy.load(std::memory_order_relaxed); }
 
 hipError_t gsdrFirFF(size_t decimation, const float* taps, size_t tapCount, const float* input, float* output,
                      size_t outputCount, int32_t device, hipStream_t stream) {

@@ -23,3 +23,18 @@ struct FirPlanShape {
 FirPlanShape planFirShape(size_t tapCount, size_t decimation);
 
 }  // namespace gsdr_amd
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace gsdr_amd {
+
+// int8 IQ -> FC FIR on the exact int8 MFMA path (fir_i8_mfma.hip).
+bool firI8MfmaEligible(size_t tapCount, size_t decimation, const void* in);
+hipError_t launchFirI8Mfma(const int8_t* iq, const float* taps, size_t tapCount, void* out, size_t nOut, int epi,
+                           hipStream_t stream);
+
+// Kernel-selection policy bits (gsdrAmdSetKernelPolicy).
+uint32_t kernelPolicy();
+
+}  // namespace gsdr_amd

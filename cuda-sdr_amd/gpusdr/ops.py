@@ -6,6 +6,8 @@ reference entry point (argument meaning and the FIR count rule of src/filters/Fi
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from ._native import check, lib
@@ -138,3 +140,16 @@ def synth_wideband_cf32(seed: int, f1: float, f2: float, first: int, n: int,
     check(lib().gsdrSynthWidebandCf32(seed, f1, f2, first, out.data_ptr(), n, _dev(out), _stream(out)),
           "gsdrSynthWidebandCf32")
     return out
+
+
+POLICY_NO_MFMA = 1  # include/gsdr/gsdr_amd.h GSDR_POLICY_NO_MFMA
+
+
+def set_kernel_policy(flags: int) -> int:
+    """Set the process-wide kernel-selection policy; returns the previous flags."""
+    L = lib()
+    L.gsdrAmdGetKernelPolicy.restype = ctypes.c_uint32
+    L.gsdrAmdSetKernelPolicy.argtypes = [ctypes.c_uint32]
+    prev = L.gsdrAmdGetKernelPolicy()
+    L.gsdrAmdSetKernelPolicy(flags)
+    return prev

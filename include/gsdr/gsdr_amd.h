@@ -49,6 +49,14 @@ GSDR_API hipError_t gsdrFirCCAmDemod(size_t decimation, const hipFloatComplex* t
  *   f1, f2 in cycles per sample.
  * Phases are reduced in double precision (n mod period) before the float trig.
  */
+/*
+ * Kernel-selection policy (process-wide; default 0). GSDR_POLICY_NO_MFMA routes the int8 IQ
+ * FIR through the fp32 VALU kernel instead of the exact int8 MFMA kernel (A/B comparisons).
+ */
+#define GSDR_POLICY_NO_MFMA 1u
+GSDR_API void gsdrAmdSetKernelPolicy(uint32_t flags);
+GSDR_API uint32_t gsdrAmdGetKernelPolicy(void);
+
 GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
                                     uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,
                                     hipStream_t stream);

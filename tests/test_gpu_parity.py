@@ -149,7 +149,9 @@ def test_am_demod_bit_exact(ops, orc, golden_dir):
 
 @pytest.mark.parametrize("T,D", [(127, 1), (1023, 10), (255, 20), (5, 1)])
 def test_fused_chains_match_unfused_bit_exact(ops, orc, T, D):
-    """int8 -> FIR -> AM in one kernel == gsdrInt8ToNormFloat -> gsdrFirFC -> gsdrQuadAmDemod."""
+    """On the fp32 VALU path, int8 -> FIR -> AM in one kernel == gsdrInt8ToNormFloat ->
+    gsdrFirFC -> gsdrQuadAmDemod bit for bit. (The int8 MFMA path is checked against the oracle
+    in test_int8_mfma_path.)"""
     import torch
     rng = np.random.default_rng(T + D)
     n_out = 5000
@@ -157,19 +159,64 @@ def test_fused_chains_match_unfused_bit_exact(ops, orc, T, D):
     iq = rng.integers(-128, 128, size=2 * n_in).astype(np.int8)
     taps = orc.lowpass_taps(T, 0.2 / D if D > 1 else 0.1)
     iq_d, taps_d = _dev(iq), _dev(taps)
-    xf = ops.int8_to_norm_float(iq_d).view(torch.complex64)
-    y_unfused = ops.fir(taps_d, xf, D, n_out)
-    am_unfused = ops.quad_am_demod(y_unfused)
-    y_fused = ops.fir(taps_d, iq_d, D, n_out, int8_iq=True)
-    am_fused = ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=True)
-    am_fir_fused = ops.fir(taps_d, xf, D, n_out, am=True)
-    assert _host(y_fused).tobytes() == _host(y_unfused).tobytes()
-    assert _host(am_fused).tobytes() == _host(am_unfused).tobytes()
-    assert _host(am_fir_fused).tobytes() == _host(am_unfused).tobytes()
+    prev = ops.set_kernel_policy(ops.POLICY_NO_MFMA)
+    try:
+        xf = ops.int8_to_norm_float(iq_d).view(torch.complex64)
+        y_unfused = ops.fir(taps_d, xf, D, n_out)
+        am_unfused = ops.quad_am_demod(y_unfused)
+        y_fused = ops.fir(taps_d, iq_d, D, n_out, int8_iq=True)
+        am_fused = ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=True)
+        am_fir_fused = ops.fir(taps_d, xf, D, n_out, am=True)
+        assert _host(y_fused).tobytes() == _host(y_unfused).tobytes()
+        assert _host(am_fused).tobytes() == _host(am_unfused).tobytes()
+        assert _host(am_fir_fused).tobytes() == _host(am_unfused).tobytes()
+    finally:
+        ops.set_kernel_policy(prev)
     # and against the float64 oracle
     x = orc.int8_to_float(iq).view(np.complex64)
     y64, bound = orc.fir_f64(taps, x, D, n_out)
     assert np.all(np.abs(_host(am_fused) - np.abs(y64)) <= FIR_TOL * bound + 1e-30)
+
+
+MFMA_CASES = [(1, 1), (2, 7), (31, 2048), (32, 2049), (33, 4095), (63, 777), (64, 65536), (65, 3),
+              (96, 10000), (127, 50000), (128, 2047), (129, 123457)]
+
+
+@pytest.mark.parametrize("T,n_out", MFMA_CASES)
+def test_int8_mfma_path(ops, orc, T, n_out):
+    """Exact int8 MFMA FIR (D = 1, T <= 129): against the float64 oracle, AM consistent with the
+    complex output bit for bit, and against the fp32 VALU kernel within the tolerance."""
+    import torch
+    rng = np.random.default_rng(T * 7 + n_out)
+    n_in = n_out - 1 + T
+    iq = rng.integers(-128, 128, size=2 * n_in).astype(np.int8)
+    iq[:64] = -128  # the clamp -128 -> -127 must be exact
+    taps = (orc.lowpass_taps(T, 0.1) if T > 2 else rng.standard_normal(T)).astype(np.float32)
+    taps[T // 2] *= -1.5
+    iq_d, taps_d = _dev(iq), _dev(taps)
+    y = _host(ops.fir(taps_d, iq_d, 1, n_out, int8_iq=True))
+    am = _host(ops.fir(taps_d, iq_d, 1, n_out, int8_iq=True, am=True))
+    x = orc.int8_to_float(iq).view(np.complex64)
+    y64, bound = orc.fir_f64(taps, x, 1, n_out)
+    _check_fir(y, y64, bound, ("mfma", T, n_out))
+    assert am.tobytes() == orc.quad_am_demod(y).tobytes()
+    prev = ops.set_kernel_policy(ops.POLICY_NO_MFMA)
+    try:
+        y_valu = _host(ops.fir(taps_d, iq_d, 1, n_out, int8_iq=True))
+    finally:
+        ops.set_kernel_policy(prev)
+    assert np.all(np.abs(y.astype(np.complex128) - y_valu) <= 2 * FIR_TOL * bound + 1e-30)
+    del torch
+
+
+def test_int8_mfma_misaligned_falls_back(ops, orc):
+    rng = np.random.default_rng(77)
+    T, n_out = 127, 3000
+    iq = rng.integers(-128, 128, size=2 * (n_out + T) + 2).astype(np.int8)
+    taps = orc.lowpass_taps(T, 0.1)
+    y = _host(ops.fir(_dev(taps), _dev(iq)[2:], 1, n_out, int8_iq=True))  # 2-byte offset: VALU path
+    y64, bound = orc.fir_f64(taps, orc.int8_to_float(iq[2:]).view(np.complex64), 1, n_out)
+    _check_fir(y, y64, bound, "misaligned")
 
 
 def test_cosine_sources(ops, orc):
