@@ -212,11 +212,12 @@ def test_int8_mfma_path(ops, orc, T, n_out):
 def test_int8_mfma_misaligned_falls_back(ops, orc):
     rng = np.random.default_rng(77)
     T, n_out = 127, 3000
-    iq = rng.integers(-128, 128, size=2 * (n_out + T) + 2).astype(np.int8)
+    iq = rng.integers(-128, 128, size=2 * (n_out + T) + 8).astype(np.int8)
     taps = orc.lowpass_taps(T, 0.1)
-    y = _host(ops.fir(_dev(taps), _dev(iq)[2:], 1, n_out, int8_iq=True))  # 2-byte offset: VALU path
-    y64, bound = orc.fir_f64(taps, orc.int8_to_float(iq[2:]).view(np.complex64), 1, n_out)
-    _check_fir(y, y64, bound, "misaligned")
+    for off in (2, 4, 6):  # 2-, 4-, 2-byte aligned starts: the ushort / dword staging variants
+        y = _host(ops.fir(_dev(taps), _dev(iq)[off:], 1, n_out, int8_iq=True))
+        y64, bound = orc.fir_f64(taps, orc.int8_to_float(iq[off:]).view(np.complex64), 1, n_out)
+        _check_fir(y, y64, bound, ("misaligned", off))
 
 
 def test_cosine_sources(ops, orc):
