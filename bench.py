@@ -7,6 +7,10 @@ One step = one second of signal per GPU (20 M IQ samples), inputs resident in HB
 The whole chain runs as the fused gfx950 kernel gsdrInt8FirFCAmDemod (== the chain
 gsdrInt8ToNormFloat -> gsdrFirFC -> gsdrQuadAmDemod, bit for bit; tests/test_gpu_parity.py).
 
+One GPU: the step is ONE launch over the buffer [T-1 history | segment] that also writes the
+history for the next step (gsdrInt8FirFCAmDemodCarry; for T <= 129, D = 1 the exact int8 MFMA
+kernel firI8MfmaKernel).
+
 Multi-GPU (one process per GPU, torch.distributed over RCCL): the stream is time-sharded.
 In step s rank g owns stream samples [(s*G + g)*L, (s*G + g + 1)*L) and needs the
 preceding T-1 samples as a halo, which live on rank g-1 (rank 0: rank G-1's segment of the
@@ -38,6 +42,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "Msamples/sec through FIR→QuadAmDemod chain at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, spec
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md, FP32 vector (packed FMA)
+INT8_PEAK_TOPS = 5000.0        # MI355X_MICROARCH.md, I8 MFMA dense (2x the BF16 rate)
 
 WORKLOADS = {
     # name: (description, input kind, samples per GPU step, taps, decimation, cutoff, window, fs)
@@ -103,6 +108,12 @@ class ShardedChain:
         if n_out > 0:
             self.ops.fir(self.taps, x, self.D, n_out, out=out, am=True, int8_iq=(self.kind == "i8"))
 
+    @property
+    def single(self):
+        """World 1: the whole step is ONE launch over [history | segment]; for int8 IQ the
+        history carry for the next step is fused into it (gsdrInt8FirFCAmDemodCarry)."""
+        return self.geom.world == 1
+
     def bulk(self):
         """Outputs [head, L/D): inputs entirely inside this rank's segment (the timed kernel)."""
         g = self.geom
@@ -118,14 +129,36 @@ class ShardedChain:
 
     def step(self, ev=None):
         self.ev = ev
-        self.ring.step(self.bulk, self.head)
-
-    def bulk_bytes_flops(self):
+        if not self.single:
+            self.ring.step(self.bulk, self.head)
+            return
         g = self.geom
-        n = g.outputs - g.head_outputs
+        if ev is not None:
+            ev[0].record()
+        if self.kind == "i8":
+            self.ops.fir_am_i8_carry(self.taps, self.buf, self.D, g.outputs, self.out, self.ring.halo)
+        else:
+            self._fir(self.buf, g.outputs, self.out)
+        if ev is not None:
+            ev[1].record()
+        if self.kind != "i8":
+            self.ring.halo.copy_(self.ring.tail)
+
+    def timed_bytes_ops(self):
+        """Algorithmic bytes of the timed launch (input read once + output written once) and
+        its arithmetic: int8 MFMA ops for the exact int8 kernel, direct-form FMA flops else."""
+        g = self.geom
+        n = g.outputs if self.single else g.outputs - g.head_outputs
         n_in = (n - 1) * self.D + self.T
         in_bytes = n_in * (2 if self.kind == "i8" else 8)
-        return in_bytes + n * 4, n * self.T * 4  # algorithmic bytes; direct-form FC flops
+        if self.mfma_int8:
+            s = (self.T + 62) // 32  # K-steps of 32: K = 32 S >= T + 31
+            return in_bytes + n * 4, n * 2 * 4 * 32 * s * 2  # I and Q rows x 4 limbs x K MACs x 2
+        return in_bytes + n * 4, n * self.T * 4
+
+    @property
+    def mfma_int8(self):
+        return self.kind == "i8" and self.D == 1 and self.T <= 129
 
 
 def cpu_baseline(wl, seconds_target=8.0):
@@ -164,6 +197,13 @@ def cpu_baseline(wl, seconds_target=8.0):
         "sample": f"{n_out * D} input samples of the {wl} chain (oracle/gsdr_oracle.c float32 direct form, "
                   f"{threads} threads, mean of {reps} runs)",
     }
+
+
+def kernel_name(chain):
+    entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
+        else "gsdrFirFCAmDemod"
+    body = "firI8MfmaKernel" if chain.mfma_int8 else "firLdsKernel"
+    return f"{entry} ({body})"
 
 
 def load_traffic(wl):
@@ -212,9 +252,9 @@ def main():
         elapsed = float(t.item())
 
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    bytes_, flops = chain.bulk_bytes_flops()
+    bytes_, ops_ = chain.timed_bytes_ops()
     achieved_gbs = bytes_ / (kernel_ms * 1e-3) / 1e9
-    achieved_tf = flops / (kernel_ms * 1e-3) / 1e12
+    achieved_t = ops_ / (kernel_ms * 1e-3) / 1e12
     total_samples = world * chain.L * args.steps
     value = total_samples / elapsed / 1e6
 
@@ -248,7 +288,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "gsdrInt8FirFCAmDemod (firLdsKernel)" if chain.kind == "i8" else "gsdrFirFCAmDemod",
+                "kernel": kernel_name(chain),
                 "achieved": achieved_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -256,9 +296,12 @@ def main():
                 "traffic": traffic,
                 "avg_launch_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": bytes_,
-                "fp32_valu": {"achieved_tflops": achieved_tf, "peak_tflops": FP32_PEAK_TFLOPS,
-                              "frac": achieved_tf / FP32_PEAK_TFLOPS,
-                              "flops_per_launch": flops},
+                "compute": ({"kind": "int8 MFMA (4 tap limbs)", "achieved_tops": achieved_t,
+                             "peak_tops": INT8_PEAK_TOPS, "frac": achieved_t / INT8_PEAK_TOPS,
+                             "ops_per_launch": ops_} if chain.mfma_int8 else
+                            {"kind": "fp32 VALU FMA", "achieved_tflops": achieved_t,
+                             "peak_tflops": FP32_PEAK_TFLOPS, "frac": achieved_t / FP32_PEAK_TFLOPS,
+                             "flops_per_launch": ops_}),
             },
             "cpu_baseline": cpu,
         }

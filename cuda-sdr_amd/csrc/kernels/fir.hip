@@ -519,6 +519,37 @@ hipError_t gsdrInt8FirFCAmDemod(size_t decimation, const float* taps, size_t tap
                                             stream);
 }
 
+hipError_t gsdrInt8FirFCAmDemodCarry(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
+                                     float* output, size_t outputCount, int8_t* carryIq, int32_t device,
+                                     hipStream_t stream) {
+  if (outputCount == 0) return hipSuccess;
+  const size_t d = decimation < 1 ? 1 : decimation;
+  const size_t carry = tapCount > d ? tapCount - d : 0;  // samples from outputCount * d on
+  if (inputIq == nullptr || (carry > 0 && carryIq == nullptr)) return hipErrorInvalidValue;
+  if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firI8MfmaEligible(tapCount, decimation, inputIq) &&
+      outputCount + 1 >= tapCount && taps != nullptr && output != nullptr) {
+    DevicePush push(device);
+    if (!push.ok) return hipErrorInvalidDevice;
+    return launchFirI8Mfma(inputIq, taps, tapCount, output, outputCount, kEpiAm, stream,
+                           carry > 0 ? carryIq : nullptr);
+  }
+  hipError_t e = launchFir<kFirFC, kInI8IQ, kEpiAm>(inputIq, taps, tapCount, decimation, output, outputCount, device,
+                                                    stream);
+  if (e != hipSuccess || carry == 0) return e;
+  DevicePush push(device);
+  if (!push.ok) return hipErrorInvalidDevice;
+  const int8_t* src = inputIq + 2 * outputCount * d;
+  const size_t bytes = 2 * carry;
+  const bool overlap = src < carryIq + bytes && carryIq < src + bytes;
+  if (!overlap) return hipMemcpyAsync(carryIq, src, bytes, hipMemcpyDeviceToDevice, stream);
+  void* tmp = nullptr;  // overlapping history (short pushes): bounce through a temporary
+  if ((e = hipMallocAsync(&tmp, bytes, stream)) != hipSuccess) return e;
+  e = hipMemcpyAsync(tmp, src, bytes, hipMemcpyDeviceToDevice, stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(carryIq, tmp, bytes, hipMemcpyDeviceToDevice, stream);
+  const hipError_t f = hipFreeAsync(tmp, stream);
+  return e != hipSuccess ? e : f;
+}
+
 hipError_t gsdrFirCCAmDemod(size_t decimation, const hipFloatComplex* taps, size_t tapCount,
                             const hipFloatComplex* input, float* output, size_t outputCount, int32_t device,
                             hipStream_t stream) {

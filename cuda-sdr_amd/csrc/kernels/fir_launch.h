@@ -31,8 +31,10 @@ namespace gsdr_amd {
 
 // int8 IQ -> FC FIR on the exact int8 MFMA path (fir_i8_mfma.hip).
 bool firI8MfmaEligible(size_t tapCount, size_t decimation, const void* in);
+// carryDst != nullptr: the launch also copies the last tapCount - 1 input samples there (the
+// streaming history); it may alias the first tapCount - 1 input samples. Needs nOut >= tapCount - 1.
 hipError_t launchFirI8Mfma(const int8_t* iq, const float* taps, size_t tapCount, void* out, size_t nOut, int epi,
-                           hipStream_t stream);
+                           hipStream_t stream, int8_t* carryDst = nullptr);
 
 // Kernel-selection policy bits (gsdrAmdSetKernelPolicy).
 uint32_t kernelPolicy();

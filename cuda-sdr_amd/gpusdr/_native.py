@@ -45,6 +45,8 @@ def _declare(L):
         fn = getattr(L, name)
         fn.argtypes = fir_sig
         fn.restype = err
+    L.gsdrInt8FirFCAmDemodCarry.argtypes = [sz, vp, sz, vp, vp, sz, vp, i32, vp]
+    L.gsdrInt8FirFCAmDemodCarry.restype = err
     for name in ("gsdrQuadAmDemod", "gsdrInt8ToNormFloat", "gsdrFloatToInt8"):
         fn = getattr(L, name)
         fn.argtypes = [vp, vp, sz, i32, vp]

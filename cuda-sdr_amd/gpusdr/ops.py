@@ -91,6 +91,26 @@ def fir(taps: torch.Tensor, x: torch.Tensor, decimation: int = 1, num_outputs: i
     return out
 
 
+def fir_am_i8_carry(taps: torch.Tensor, iq: torch.Tensor, decimation: int, num_outputs: int,
+                    out: torch.Tensor, carry: torch.Tensor) -> torch.Tensor:
+    """Streaming int8 IQ -> FIR -> AM (gsdrInt8FirFCAmDemodCarry): writes `num_outputs` AM
+    samples to `out` and, in the same launch, copies the history the next call needs (the last
+    T - D input samples) to `carry`, which may be a view of the start of `iq` (in-place history)."""
+    _require(taps, torch.float32, "taps")
+    _require(iq, torch.int8, "iq")
+    _require(out, torch.float32, "out")
+    _require(carry, torch.int8, "carry")
+    d = max(1, int(decimation))
+    T = taps.numel()
+    if num_outputs > 0 and (num_outputs - 1) * d + T > iq.numel() // 2:
+        raise ValueError("input too short for the requested outputs")
+    if out.numel() < num_outputs or carry.numel() < 2 * max(0, T - d):
+        raise ValueError("out or carry too small")
+    check(lib().gsdrInt8FirFCAmDemodCarry(d, taps.data_ptr(), T, iq.data_ptr(), out.data_ptr(), num_outputs,
+                                          carry.data_ptr(), _dev(iq), _stream(iq)), "gsdrInt8FirFCAmDemodCarry")
+    return out
+
+
 def quad_am_demod(z: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _require(z, torch.complex64, "z")
     if out is None:

@@ -36,6 +36,18 @@ GSDR_API hipError_t gsdrFirCCAmDemod(size_t decimation, const hipFloatComplex* t
                                      hipStream_t stream);
 
 /*
+ * Streaming form of gsdrInt8FirFCAmDemod: the same outputs, and the history the next call needs
+ * (input samples [outputCount * decimation, (outputCount - 1) * decimation + tapCount), i.e. the
+ * last tapCount - decimation samples) is copied to carryIq in the same launch. carryIq may alias
+ * the start of inputIq - the in-place layout [history | new samples] of a streaming FIR, where the
+ * next block of samples is then written right behind the carried history. It must not alias
+ * any other part of inputIq or the output.
+ */
+GSDR_API hipError_t gsdrInt8FirFCAmDemodCarry(size_t decimation, const float* taps, size_t tapCount,
+                                              const int8_t* inputIq, float* output, size_t outputCount,
+                                              int8_t* carryIq, int32_t device, hipStream_t stream);
+
+/*
  * Deterministic synthetic sources for the benchmark configurations.
  * Sample n (absolute stream index firstSample + i) depends only on (seed, n), so a
  * time-sharded stream is generated shard by shard with no communication.

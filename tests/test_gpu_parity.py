@@ -199,7 +199,9 @@ def test_int8_mfma_path(ops, orc, T, n_out):
     x = orc.int8_to_float(iq).view(np.complex64)
     y64, bound = orc.fir_f64(taps, x, 1, n_out)
     _check_fir(y, y64, bound, ("mfma", T, n_out))
-    assert am.tobytes() == orc.quad_am_demod(y).tobytes()
+    # the MFMA epilogue takes the hardware square root (v_sqrt_f32, <= 1 ulp)
+    am_ref = orc.quad_am_demod(y)
+    assert np.all(np.abs(am - am_ref) <= np.spacing(am_ref))
     prev = ops.set_kernel_policy(ops.POLICY_NO_MFMA)
     try:
         y_valu = _host(ops.fir(taps_d, iq_d, 1, n_out, int8_iq=True))
@@ -212,12 +214,43 @@ def test_int8_mfma_path(ops, orc, T, n_out):
 def test_int8_mfma_misaligned_falls_back(ops, orc):
     rng = np.random.default_rng(77)
     T, n_out = 127, 3000
-    iq = rng.integers(-128, 128, size=2 * (n_out + T) + 8).astype(np.int8)
+    iq = rng.integers(-128, 128, size=2 * (n_out + T) + 16).astype(np.int8)
     taps = orc.lowpass_taps(T, 0.1)
-    for off in (2, 4, 6):  # 2-, 4-, 2-byte aligned starts: the ushort / dword staging variants
+    for off in (2, 4, 6, 14):  # every even misalignment class of the split pass
         y = _host(ops.fir(_dev(taps), _dev(iq)[off:], 1, n_out, int8_iq=True))
         y64, bound = orc.fir_f64(taps, orc.int8_to_float(iq[off:]).view(np.complex64), 1, n_out)
         _check_fir(y, y64, bound, ("misaligned", off))
+
+
+@pytest.mark.parametrize("T,L,mfma", [(127, 10000, True), (127, 50, True), (33, 4099, True), (127, 10000, False),
+                                       (1, 300, True)])
+def test_fir_carry_streaming(ops, orc, T, L, mfma):
+    """gsdrInt8FirFCAmDemodCarry over a stream pushed in blocks of L samples into one buffer
+    [history | block]: the in-place history carry makes the concatenated outputs those of one
+    FIR over the whole stream. L = 50 < T - 1 takes the overlapping (bounce) carry."""
+    import torch
+    rng = np.random.default_rng(T * 3 + L)
+    nblk, H = 5, T - 1
+    stream = rng.integers(-128, 128, size=2 * (H + nblk * L)).astype(np.int8)
+    taps = (orc.lowpass_taps(T, 0.1) if T > 2 else np.ones(T)).astype(np.float32)
+    taps_d = _dev(taps)
+    buf = torch.zeros(2 * (H + L), dtype=torch.int8, device="cuda")
+    buf[: 2 * H] = _dev(stream[: 2 * H])
+    prev = ops.set_kernel_policy(0 if mfma else ops.POLICY_NO_MFMA)
+    outs = []
+    try:
+        for b in range(nblk):
+            buf[2 * H:] = _dev(stream[2 * (H + b * L): 2 * (H + (b + 1) * L)])
+            out = torch.empty(L, dtype=torch.float32, device="cuda")
+            ops.fir_am_i8_carry(taps_d, buf, 1, L, out, buf[: 2 * H])
+            outs.append(_host(out))
+    finally:
+        ops.set_kernel_policy(prev)
+    am = np.concatenate(outs)
+    x = orc.int8_to_float(stream).view(np.complex64)
+    y64, bound = orc.fir_f64(taps, x, 1, nblk * L)
+    assert np.all(np.abs(am - np.abs(y64)) <= FIR_TOL * bound + 1e-30), (T, L, mfma)
+    assert _host(buf[: 2 * H]).tobytes() == stream[len(stream) - 2 * H:].tobytes()
 
 
 def test_cosine_sources(ops, orc):

@@ -28,11 +28,7 @@ case "$WHAT" in
   *bench*|all) step bench 600 python bench.py --steps 30 --warmup 5 ;;&
   *prof*|all)  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                   python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;&
-  *pmc*|all)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-                  python bench.py --steps 5 --warmup 1 --no-cpu-baseline
-               step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-                  python bench.py --steps 5 --warmup 1 --no-cpu-baseline
-               python tools/pmc_traffic.py c2 "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_traffic.json" ;;&
+  *pmc*|all)   step pmc 1100 bash tools/pmc_session.sh c2 ;;&
   *) ;;
 esac
 echo "session done"

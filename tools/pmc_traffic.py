@@ -33,7 +33,8 @@ def dominant(rows):
         return None
     gmax = max(r[1] for r in fir)
     vals = [r[2] for r in fir if r[1] == gmax]
-    return {"kernel": fir[0][0], "grid_threads": gmax, "launches": len(vals), "mean_kib": sum(vals) / len(vals)}
+    name = next(r[0] for r in fir if r[1] == gmax)
+    return {"kernel": name, "grid_threads": gmax, "launches": len(vals), "mean_kib": sum(vals) / len(vals)}
 
 
 def main(workload, fetch_dir, write_dir, out=None):
