@@ -48,8 +48,8 @@ WORKLOADS = {
     # name: (description, input kind, samples per GPU step, taps, decimation, cutoff, window, fs)
     "c2": ("C2: HackRF int8 IQ @20 Msps -> cf32 -> 127-tap FC FIR -> QuadAmDemod, 1 s per GPU step",
            "i8", 20_000_000, 127, 1, 0.1, "hamming", 20e6),
-    "c3": ("C3: wideband cf32 @200 Msps, 2^28 samples -> 1023-tap FC FIR, D=10 -> QuadAmDemod",
-           "c64", 1 << 28, 1023, 10, 0.04, "blackman", 200e6),
+    "c3": ("C3: wideband cf32 @200 Msps, 2^28 - 6 samples (a multiple of D) -> 1023-tap FC FIR, D=10 -> QuadAmDemod",
+           "c64", (1 << 28) - (1 << 28) % 10, 1023, 10, 0.04, "blackman", 200e6),
     "c4": ("C4: cf32 stream, 1023-tap FC FIR, D=1 -> QuadAmDemod, 2^26 samples per GPU step",
            "c64", 1 << 26, 1023, 1, 0.04, "blackman", 1e9),
 }

@@ -1,61 +1,65 @@
-// Exact int8 MFMA FIR for interleaved int8 IQ input (the C2 chain: int8 IQ -> cf32 -> FC FIR
-// [-> AM envelope]), decimation 1, up to 129 real taps.
+// MFMA FIR for interleaved int8 IQ input (the C2 chain: int8 IQ -> cf32 -> FC FIR [-> AM
+// envelope]), decimation 1, up to 129 real taps.
 //
 // Arithmetic. gsdrInt8ToNormFloat maps x to fmaxf(-1, x/127) = x'/127 with x' = max(x, -127), so
 //     y[k] = sum_j h_j x'[k+j] / 127.
-// The taps are quantised once to a 30-bit fixed point H_j = rint(h_j 2^sc) (sc from max|h|, error
-// <= max|h| 2^-31 per tap) and split into four signed base-256 digits (limbs) H = L0 + L1 2^8 +
-// L2 2^16 + L3 2^24, |L| <= 128. Every sum_j L_lj x'[k+j] is then an EXACT int32 dot product of
-// int8 values - what v_mfma_i32_32x32x32_i8 computes - and
-//     y = ((S0 + S1 2^8) + (S2 + S3 2^8) 2^16) 2^-sc / 127
-// is rounded once or twice in fp32. The result is closer to the float64 oracle than the fp32
-// direct form (error ~1e-7 of sum|h||x| vs ~T^0.5 eps); tests/test_gpu_parity.py checks it.
+// x' is an integer in [-127, 127]: exact in f16. The taps are scaled by a block-uniform power of
+// two 2^sc (max |h 2^sc| in [2^14, 2^15)) and split into two f16 limbs, hs = hi + lo + e with
+// hi = f16(hs), lo = f16(hs - hi), |e| <= 2^-22 |hs| (2^-25 absolute once lo is subnormal, i.e.
+// below 2^-39 of the largest tap). v_mfma_f32_32x32x16_f16 forms the products x' * limb exactly
+// and accumulates both limbs into ONE fp32 accumulator, so
+//     y = acc * 2^-sc / 127
+// carries the rounding of an fp32 accumulation of exact terms - the same class as the fp32
+// direct form the reference computes; tests/test_gpu_parity.py bounds it against float64.
 //
 // GEMM shape (Toeplitz). Output k = 32 m + n (row m, column n < 32):
 //     C[m][n] = sum_kappa A[m][kappa] B[kappa][n],  A[m][kappa] = x'[32 m + kappa],
-//     B[kappa][n] = H[kappa - n] (0 <= kappa - n < T, else 0),  kappa < K = 32 S >= T + 31.
-// One 32x32x32 MFMA tile holds 16 rows of the I stream and the same 16 rows of the Q stream
-// (A rows 0-15 read the I plane, rows 16-31 the Q plane), so a lane ends with I and Q of the
-// same output in registers i and i+8: the AM envelope needs no data movement.
-// Per wave tile: 512 complex outputs = S K-steps x 4 limbs MFMAs; the B fragments (taps) live in
-// registers for the whole kernel (16 S VGPRs), the A fragment is one ds_read_b128 per K-step
-// from the block's staged, clamped, I/Q-deinterleaved LDS window.
+//     B[kappa][n] = h[kappa - n] (0 <= kappa - n < T, else 0),  kappa < K = 32 S >= T + 31.
+// One 32x32 MFMA tile holds 16 rows of the I stream and the same 16 rows of the Q stream (A
+// rows 0-15 read the I plane, rows 16-31 the Q plane), so a lane ends with I and Q of the same
+// output in accumulator registers i and i+8: the AM envelope needs no data movement.
+// Per wave tile: 512 complex outputs = S K-blocks x 2 K-halves (16 each) x 2 limbs MFMAs; the B
+// fragments (taps) live in registers for the whole kernel (16 S VGPRs), the A fragments are
+// ds_read_b128 from the block's f16 I/Q planes. Only the consistency of the lane -> k map of A
+// and B matters (a dot product is invariant under a common permutation of k).
 //
-// Cost per complex output: 4 limbs x K/32 MFMA-cycles: at T = 127 (S = 5) 1.25 SIMD-cycles per
-// output, ~2 Tsamples/s of MFMA throughput on 1024 SIMDs - above the ~1 Tsample/s the
-// 6-byte-per-sample HBM stream allows, so the chain becomes HBM-bound.
+// Cost: 4 S MFMAs of 32 cycles per 512 outputs: at T = 127 (S = 5) 1.25 SIMD-cycles per output
+// (~10 us of matrix-core time for 20 M outputs), below the ~20 us the 6-byte-per-sample HBM
+// stream takes; the epilogue is 4 VALU operations per output.
 //
-// Data movement (v3). Each block owns a contiguous range of 4096-output chunks (its windows
-// overlap by T - 1 samples, so the overlap is an L2 hit). The raw interleaved window of a chunk
-// goes HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPRs) into a ring of kRing slots
-// filled kRing - 1 chunks ahead, so ~25 KB of loads per block stay in flight across the MFMA
-// work and the barriers; one pass per chunk then clamps and splits the slot into the I / Q
-// planes the A fragments read. The DMA is issued from inline asm and retired with counted
-// `s_waitcnt vmcnt(N)` (the compiler does not see it): N counts the DMA pieces and the epilogue
-// stores issued after the slot being waited for (see vmWaitFor).
+// Data movement. Each block owns a contiguous range of 4096-output chunks (their windows
+// overlap by T - 1 samples, an L2 hit). The raw interleaved window of a chunk goes HBM -> LDS by
+// LDS-DMA (global_load_lds_dwordx4, no VGPRs) into a ring of kRing slots filled kRing - 1 chunks
+// ahead, so the loads of the next chunks stay in flight across the MFMA work and the barriers;
+// one pass per chunk then clamps, converts and splits the slot into the f16 I / Q planes. The
+// DMA is issued from inline asm and retired with counted `s_waitcnt vmcnt(N)` (the compiler
+// does not see it): N counts the DMA pieces and the epilogue stores issued after the slot waited
+// for.
 #include "kcommon.h"
 #include "fir_launch.h"
 
 namespace gsdr_amd {
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int kI8Waves = 4;
 constexpr int kI8Threads = kI8Waves * kWave;
-constexpr int kI8TileOut = 512;                                   // 16 rows x 32 columns
+constexpr int kI8TileOut = 512;                                        // 16 rows x 32 columns
 constexpr int kI8TilesPerWave = 2;
 constexpr int kI8ChunkOut = kI8Waves * kI8TilesPerWave * kI8TileOut;  // 4096 outputs per chunk
-constexpr int kI8MaxS = 5;                                        // K <= 160 -> T <= 129
-constexpr int kRing = 4;                                          // LDS-DMA ring slots
-constexpr int kPiece = 64 * 16;                                   // bytes per wave DMA instruction
+constexpr int kI8MaxS = 5;                                             // K <= 160 -> T <= 129
+constexpr int kRing = 3;                                               // LDS-DMA ring slots
+constexpr int kPiece = 64 * 16;                                        // bytes per wave DMA instruction
+constexpr int kRingPad = 16;                                           // room for the DMA re-alignment
 // Epilogue stores per wave per chunk (one store instruction per lane output, 8 per tile).
 constexpr int kStoresPerChunk = kI8TilesPerWave * 8;
 
-// Lane -> k map of the 16 bytes of an A / B fragment of v_mfma_i32_32x32x32_i8. Only its
-// consistency between A and B matters (a dot product is invariant under a common permutation
-// of k); tools/probes/mfma_i8_layout.hip confirms A/B/C maps with exact integers on gfx950.
-__device__ __forceinline__ int i8FragK(int half, int j) { return 16 * half + j; }
+// Tap-limb table: 2 rows (hi, lo) of kLimbRow f16, tap j at kLimbPad + j, zero elsewhere.
+constexpr int kLimbPad = 32;
+constexpr int kLimbRow = 256;
+static_assert(kLimbPad + 32 * kI8MaxS + 16 <= kLimbRow && 2 * kLimbRow * 2 == 4 * kI8Threads, "limb table");
 
 struct I8FirArgs {
   const int8_t* iq;   // interleaved I, Q (2-byte aligned)
@@ -65,31 +69,24 @@ struct I8FirArgs {
   int64_t nIn;        // complex samples readable: nOut - 1 + T
   int32_t T;
   int32_t chunks;
-  int8_t* carryDst;     // nullptr, or where the last T - 1 input samples go (may alias iq[0 .. T-1))
+  int8_t* carryDst;   // nullptr, or where the last T - 1 input samples go (may alias iq[0 .. T-1))
 };
 
 template <int S>
 struct I8Geom {
-  static constexpr int kWin = kI8ChunkOut - 32 + 32 * S;        // samples one chunk reads
-  static constexpr int kPlane = (kWin + 15) / 16 * 16;           // bytes per I / Q plane
-  static constexpr int kGroups = kPlane / 8;                     // 8-sample staging groups
-  // slot: up to 14 bytes of alignment shift + the window + one dword of read-ahead
-  static constexpr int kPieces = (14 + 2 * kPlane + 4 + kPiece - 1) / kPiece;
+  static constexpr int kWin = kI8ChunkOut - 32 + 32 * S;  // samples one chunk reads (multiple of 32)
+  static constexpr int kBlocks = kWin / 32;                // 32-sample blocks per plane
+  static constexpr int kGroups = kWin / 8;                 // 8-sample split groups
+  // f16 plane: block b, 16-byte unit q (8 samples) at unit 5 b + q (one pad unit per block), the
+  // Q plane a multiple of 256 bytes after the I plane: every ds_read_b128 lane group of the A
+  // fragments (MI355X_MICROARCH.md, LDS) then hits 16 distinct 16-byte bank slots.
+  static constexpr int kPlaneBytes = (80 * kBlocks + 255) / 256 * 256;
+  // slot: the window + up to 12 bytes of DMA re-alignment + a dword of read-ahead
+  static constexpr int kPieces = (2 * kWin + 18 + kPiece - 1) / kPiece;
   static constexpr int kSlot = kPieces * kPiece;
 };
 
-// 0x80 (-128) -> 0x81 (-127) in every byte: fmaxf(-1, x/127) == max(x, -127)/127.
-__device__ __forceinline__ uint32_t clampMinByte(uint32_t w) {
-  const uint32_t low7 = w & 0x7F7F7F7Fu;
-  const uint32_t nonzeroLow = (low7 + 0x7F7F7F7Fu) & 0x80808080u;  // no carries: 0x7F + 0x7F < 0x100
-  const uint32_t isMin = (w & 0x80808080u) & ~nonzeroLow;
-  return w | (isMin >> 7);
-}
-
-// Tap-limb table: 4 rows of kLimbRow bytes, tap j of limb l at l * kLimbRow + kLimbPad + j.
-constexpr int kLimbPad = 32;
-constexpr int kLimbRow = 256;
-static_assert(kLimbPad + 32 * kI8MaxS + 20 <= kLimbRow && 4 * kLimbRow == 4 * kI8Threads, "limb table");
+__device__ __forceinline__ int planeUnit(int b, int q) { return 5 * b + q; }
 
 __device__ __forceinline__ float loadF32Async(const float* p) {
   float v;
@@ -132,12 +129,13 @@ __device__ __forceinline__ void dmaPiece(const void* src, uint32_t ldsDst) {
       : "memory");
 }
 
-// Issue this wave's DMA pieces of chunk c's raw window into ring slot `slotLds` (LDS byte
-// address). Lanes past the input end re-read the last 16-byte block that holds input bytes (it
-// never crosses a page); the bytes they land only feed outputs >= nOut, which are not stored.
+// Issue this wave's DMA pieces of chunk c's raw window into the slot at `slotLds` (LDS byte
+// address, moved down by the dword part of the input's misalignment, so the window starts at
+// the slot's nominal start + (shift & 3)). Lanes past the input end re-read the last 16-byte
+// block that holds input bytes (it never crosses a page); those bytes only feed outputs >= nOut.
 template <int S>
-__device__ __forceinline__ void issueChunk(const I8FirArgs& a, uintptr_t alignedBase, uintptr_t lastBlock, int c,
-                                           uint32_t slotLds, int wave, int lane) {
+__device__ __forceinline__ void issueChunk(uintptr_t alignedBase, uintptr_t lastBlock, int c, uint32_t slotLds,
+                                           int wave, int lane) {
   using G = I8Geom<S>;
   const uintptr_t chunkBase = alignedBase + (uintptr_t)c * (2 * kI8ChunkOut);
 #pragma unroll
@@ -151,91 +149,118 @@ __device__ __forceinline__ void issueChunk(const I8FirArgs& a, uintptr_t aligned
   }
 }
 
-// Clamp and split one landed slot into the I / Q planes: group g = samples [8g, 8g + 8) of the
-// window, at slot bytes [shift + 16 g, shift + 16 g + 16).
+// Four interleaved IQ words (I0 Q0 I1 Q1 each) -> clamped f16 I and Q units (8 samples each).
+// u = x ^ 0x80 = x + 128 lands in the low byte of the f16 1024 + u (high byte 0x64); adding
+// -1152 gives x exactly, and max(., -127) is the reference's fmaxf(-1, x/127) clamp.
+__device__ __forceinline__ void splitWords(const uint32_t (&w)[4], uint4& iu, uint4& qu) {
+  const h2 bias = {(_Float16)-1152.0f, (_Float16)-1152.0f};
+  const h2 lo = {(_Float16)-127.0f, (_Float16)-127.0f};
+  uint32_t ri[4], rq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t u = w[q] ^ 0x80808080u;
+    const uint32_t pi = __builtin_amdgcn_perm(0x64646464u, u, 0x04020400u);
+    const uint32_t pq = __builtin_amdgcn_perm(0x64646464u, u, 0x04030401u);
+    h2 fi = __builtin_bit_cast(h2, pi) + bias;
+    h2 fq = __builtin_bit_cast(h2, pq) + bias;
+    fi = __builtin_elementwise_max(fi, lo);
+    fq = __builtin_elementwise_max(fq, lo);
+    ri[q] = __builtin_bit_cast(uint32_t, fi);
+    rq[q] = __builtin_bit_cast(uint32_t, fq);
+  }
+  iu = uint4{ri[0], ri[1], ri[2], ri[3]};
+  qu = uint4{rq[0], rq[1], rq[2], rq[3]};
+}
+
+// Split one landed slot into the f16 I / Q planes: group g = samples [8g, 8g + 8) of the window
+// at window bytes [16 g, 16 g + 16); `win` is 4-byte aligned when sub = 0, else 2-byte aligned.
 template <int S>
-__device__ __forceinline__ void splitSlot(const int8_t* slot, int8_t* planes, int shift, int tid) {
+__device__ __forceinline__ void splitSlot(const int8_t* win, int8_t* planes, int sub, int tid) {
   using G = I8Geom<S>;
-  const uint32_t* words = reinterpret_cast<const uint32_t*>(slot + (shift & ~3));
-  const int sub = shift & 3;  // 0 or 2
 #pragma unroll
   for (int u = 0; u < (G::kGroups + kI8Threads - 1) / kI8Threads; ++u) {
     const int g = tid + u * kI8Threads;
     if (g < G::kGroups) {
-      uint32_t d[5];
-#pragma unroll
-      for (int q = 0; q < 5; ++q) d[q] = words[4 * g + q];
       uint32_t w[4];
+      if (sub == 0) {  // kernel-uniform: 4-byte aligned input -> the window is 16-byte aligned
+        const uint4 v = *reinterpret_cast<const uint4*>(win + 16 * g);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+      } else {
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(win - 2 + 16 * g);
+        uint32_t e[5];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] = clampMinByte(__builtin_amdgcn_alignbyte(d[q + 1], d[q], sub));
-      // bytes: I0 Q0 I1 Q1 | I2 Q2 I3 Q3 | ...
-      const uint32_t i01 = __builtin_amdgcn_perm(w[1], w[0], 0x06040200u);
-      const uint32_t i23 = __builtin_amdgcn_perm(w[3], w[2], 0x06040200u);
-      const uint32_t q01 = __builtin_amdgcn_perm(w[1], w[0], 0x07050301u);
-      const uint32_t q23 = __builtin_amdgcn_perm(w[3], w[2], 0x07050301u);
-      *reinterpret_cast<uint2*>(planes + 8 * g) = uint2{i01, i23};
-      *reinterpret_cast<uint2*>(planes + G::kPlane + 8 * g) = uint2{q01, q23};
+        for (int q = 0; q < 5; ++q) e[q] = d[q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = __builtin_amdgcn_alignbyte(e[q + 1], e[q], 2);
+      }
+      uint4 iu, qu;
+      splitWords(w, iu, qu);
+      const int unit = planeUnit(g >> 2, g & 3);
+      *reinterpret_cast<uint4*>(planes + 16 * unit) = iu;
+      *reinterpret_cast<uint4*>(planes + G::kPlaneBytes + 16 * unit) = qu;
     }
   }
 }
 
-// AM epilogue: the same expression as amEnvelope with the hardware square root (v_sqrt_f32,
-// <= 1 ulp) instead of the correctly rounded sequence - the MFMA outputs are not bit-identical to
-// the fp32 chain anyway, and the 12-instruction IEEE fix-up was ~1/3 of the epilogue.
-template <int EPI>
-__device__ __forceinline__ void storeOut(void* out, int64_t k, f2 y) {
-  if (EPI == kEpiAm) reinterpret_cast<float*>(out)[k] = __builtin_amdgcn_sqrtf(fmaf(y.x, y.x, y.y * y.y));
-  else reinterpret_cast<f2*>(out)[k] = y;
-}
-
-// One 16-row x 32-column tile (512 outputs, I and Q): S K-steps x 4 limbs MFMAs, then the
-// epilogue. Exactly 8 store instructions per lane whenever the tile is complete.
-template <int S, int EPI>
-__device__ __forceinline__ void computeTile(const I8FirArgs& a, const int8_t* planes, const v4i (&bf)[S][4],
-                                            int64_t chunkOut, int tile, int lane, float outScale,
-                                            float hiScale) {
-  constexpr int kPlane = I8Geom<S>::kPlane;
-  const int half = lane >> 5;
-  const int col = lane & 31;
+// Tile MFMAs: 16 rows x 32 columns (512 outputs, I and Q) = S K-blocks x 2 K-halves x 2 limbs,
+// both limbs accumulating into one fp32 accumulator.
+template <int S>
+__device__ __forceinline__ void tileMfma(const int8_t* planes, const h8 (&bf)[S][2][2], int tile, int lane,
+                                         v16f& acc) {
+  constexpr int kPlaneBytes = I8Geom<S>::kPlaneBytes;
   const int row = lane & 31;  // A row: 0-15 read the I plane, 16-31 the Q plane
-  v16i acc[4];
-#pragma unroll
-  for (int l = 0; l < 4; ++l) acc[l] = v16i{};
-  const int8_t* rowBase = planes + (row >> 4) * kPlane + 32 * (tile * 16 + (row & 15)) + 16 * half;
+  const int half = lane >> 5;
+  const int8_t* plane = planes + (row >> 4) * kPlaneBytes;
+  const int b0 = tile * 16 + (row & 15);
+  acc = v16f{};
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    const v4i av = *reinterpret_cast<const v4i*>(rowBase + 32 * s);
 #pragma unroll
-    for (int l = 0; l < 4; ++l) acc[l] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bf[s][l], acc[l], 0, 0, 0);
-  }
-  // limbs -> float; I and Q of one output sit in registers i and i + 8 of the same lane
-  const int64_t tileOut = chunkOut + (int64_t)tile * kI8TileOut;
-  f2 y[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const f2 lo = {(float)(acc[0][i] + (acc[1][i] << 8)), (float)(acc[0][i + 8] + (acc[1][i + 8] << 8))};
-    const f2 hi = {(float)(acc[2][i] + (acc[3][i] << 8)), (float)(acc[2][i + 8] + (acc[3][i + 8] << 8))};
-    y[i] = hi * hiScale + lo * outScale;  // packed: v_pk_mul_f32 + v_pk_fma_f32
-  }
-  const int64_t rowOut = tileOut + 4 * half * 32 + col;  // output of register i: rowOut + 32 mrow(i)
-  if (tileOut + kI8TileOut <= a.nOut) {  // wave-uniform: complete tile, straight-line stores
-#pragma unroll
-    for (int i = 0; i < 8; ++i) storeOut<EPI>(a.out, rowOut + 32 * ((i & 3) + 8 * (i >> 2)), y[i]);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int64_t k = rowOut + 32 * ((i & 3) + 8 * (i >> 2));
-      if (k < a.nOut) storeOut<EPI>(a.out, k, y[i]);
+    for (int u = 0; u < 2; ++u) {
+      const h8 av = *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0 + s, 2 * u + half));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][1], acc, 0, 0, 0);
     }
   }
+}
+
+// Tile epilogue: I and Q of one output sit in registers i and i + 8 of the same lane; 8 stores
+// per lane. FULL: the whole tile exists (straight-line stores).
+template <int EPI, bool FULL>
+__device__ __forceinline__ void tileEpilogue(const I8FirArgs& a, const v16f& acc, int64_t tileOut, int lane,
+                                             float outScale) {
+  const int64_t rowOut = tileOut + 4 * (lane >> 5) * 32 + (lane & 31);  // register i: + 32 mrow(i)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t k = rowOut + 32 * ((i & 3) + 8 * (i >> 2));
+    if (FULL || k < a.nOut) {
+      if (EPI == kEpiAm) {
+        // |y| = sqrt(yi^2 + yq^2) * scale, hardware square root (<= 1 ulp)
+        const float m2 = fmaf(acc[i], acc[i], acc[i + 8] * acc[i + 8]);
+        reinterpret_cast<float*>(a.out)[k] = __builtin_amdgcn_sqrtf(m2) * outScale;
+      } else {
+        reinterpret_cast<f2*>(a.out)[k] = f2{acc[i], acc[i + 8]} * outScale;
+      }
+    }
+  }
+}
+
+template <int S, int EPI>
+__device__ __forceinline__ void computeTile(const I8FirArgs& a, const int8_t* planes, const h8 (&bf)[S][2][2],
+                                            int64_t chunkOut, int tile, int lane, float outScale) {
+  v16f acc;
+  tileMfma<S>(planes, bf, tile, lane, acc);
+  const int64_t tileOut = chunkOut + (int64_t)tile * kI8TileOut;
+  if (tileOut + kI8TileOut <= a.nOut) tileEpilogue<EPI, true>(a, acc, tileOut, lane, outScale);
+  else tileEpilogue<EPI, false>(a, acc, tileOut, lane, outScale);
 }
 
 template <int S, int EPI>
 __global__ __launch_bounds__(kI8Threads, 3) void firI8MfmaKernel(I8FirArgs a) {
   using G = I8Geom<S>;
-  __shared__ __attribute__((aligned(16))) int8_t ring[kRing * G::kSlot];
-  __shared__ __attribute__((aligned(16))) int8_t planes[2 * G::kPlane];
-  __shared__ __attribute__((aligned(16))) int8_t limbTab[4 * kLimbRow];
+  __shared__ __attribute__((aligned(16))) int8_t ring[kRingPad + kRing * G::kSlot];
+  __shared__ __attribute__((aligned(16))) int8_t planes[2 * G::kPlaneBytes];
+  __shared__ __attribute__((aligned(16))) _Float16 limbTab[2 * kLimbRow];
   __shared__ float waveMax[kI8Waves];
 
   const int tid = threadIdx.x;
@@ -257,71 +282,75 @@ __global__ __launch_bounds__(kI8Threads, 3) void firI8MfmaKernel(I8FirArgs a) {
   const int shift = (int)(base & 15u);
   const uintptr_t alignedBase = base - shift;
   const uintptr_t lastBlock = (base + 2 * (uintptr_t)a.nIn - 1) & ~(uintptr_t)15;
-  const uint32_t ringLds = waveUniform((int)(uint32_t)reinterpret_cast<uintptr_t>(ring));
+  // slot j's window starts at ring + kRingPad + j kSlot + (shift & 3): the DMA destination moves
+  // down by the dword part of the misalignment (into the previous slot's unused tail / the pad)
+  const uint32_t ringLds =
+      (uint32_t)waveUniform((int)(uint32_t)reinterpret_cast<uintptr_t>(ring)) + kRingPad - (uint32_t)(shift & ~3);
+  const int sub = shift & 3;
   // DMA instructions this wave issues per chunk
   const int perChunk = (G::kPieces - wave + kI8Waves - 1) / kI8Waves;
   constexpr int kMaxPerChunk = (G::kPieces + kI8Waves - 1) / kI8Waves;
 #pragma unroll
   for (int j = 0; j < kRing - 1; ++j)
-    if (j < n) issueChunk<S>(a, alignedBase, lastBlock, G0 + j, ringLds + j * G::kSlot, wave, lane);
-  reinterpret_cast<uint32_t*>(limbTab)[tid] = 0u;  // 4 rows x 256 bytes = one dword per thread
+    if (j < n) issueChunk<S>(alignedBase, lastBlock, G0 + j, ringLds + j * G::kSlot, wave, lane);
+  reinterpret_cast<uint32_t*>(limbTab)[tid] = 0u;  // 2 rows x 256 f16 = one dword per thread
   vmWaitDyn<0, (kRing - 1) * kMaxPerChunk>(waveUniform(min(kRing - 1, n) * perChunk));
   asm volatile("" : "+v"(hv));  // hv is defined only after the wait
   hv = tid < T ? hv : 0.0f;
 
-  // ---- taps -> 30-bit fixed point (block-uniform scale), split into signed base-256 limbs ---
+  // ---- taps -> block-uniform power-of-two scale, two f16 limbs --------------------------------
   float m = fabsf(hv);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
   if (lane == 0) waveMax[wave] = m;
   __syncthreads();
   const float maxAbs = fmaxf(fmaxf(waveMax[0], waveMax[1]), fmaxf(waveMax[2], waveMax[3]));
-  const int sc = maxAbs > 0.0f ? 29 - ilogbf(maxAbs) : 0;  // max|H| < 2^30
+  const int sc = maxAbs > 0.0f ? 14 - ilogbf(maxAbs) : 0;  // max |h 2^sc| in [2^14, 2^15)
   if (tid < T) {
-    int v = (int)rintf(ldexpf(hv, sc));
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      const int digit = l < 3 ? (int)(int8_t)(v & 0xFF) : v;  // signed base-256 digit
-      v = (v - digit) >> 8;
-      limbTab[l * kLimbRow + kLimbPad + tid] = (int8_t)digit;
-    }
+    const float hs = ldexpf(hv, sc);
+    const _Float16 hi = (_Float16)hs;
+    limbTab[kLimbPad + tid] = hi;
+    limbTab[kLimbRow + kLimbPad + tid] = (_Float16)(hs - (float)hi);
   }
   __syncthreads();
   const float outScale = ldexpf(1.0f / 127.0f, -sc);
-  const float hiScale = outScale * 65536.0f;
 
-  // ---- B fragments: bf[s][l] holds limb l of H[kappa - n] for this lane's 16 kappas ----------
-  // kappa = 32 s + i8FragK(half, j), n = col: 16 consecutive table bytes from
-  // kLimbPad + 32 s + 16 half - col (zero outside [0, T)), re-aligned with v_alignbyte.
+  // ---- B fragments: bf[s][u][l] = limb l of h[kappa - n], kappa = 32 s + 16 u + 8 half + j -----
   const int half = lane >> 5;
   const int col = lane & 31;
-  v4i bf[S][4];
+  h8 bf[S][2][2];
 #pragma unroll
   for (int s = 0; s < S; ++s) {
-    const int b0 = kLimbPad + 32 * s + i8FragK(half, 0) - col;
 #pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(limbTab + l * kLimbRow + (b0 & ~3));
-      uint32_t d[5];
+    for (int u = 0; u < 2; ++u) {
+      const int e0 = kLimbPad + 32 * s + 16 * u + 8 * half - col;  // first f16 element
 #pragma unroll
-      for (int q = 0; q < 5; ++q) d[q] = wsrc[q];
-      bf[s][l] = v4i{(int)__builtin_amdgcn_alignbyte(d[1], d[0], b0 & 3),
-                     (int)__builtin_amdgcn_alignbyte(d[2], d[1], b0 & 3),
-                     (int)__builtin_amdgcn_alignbyte(d[3], d[2], b0 & 3),
-                     (int)__builtin_amdgcn_alignbyte(d[4], d[3], b0 & 3)};
+      for (int l = 0; l < 2; ++l) {
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(limbTab + l * kLimbRow + (e0 & ~1));
+        uint32_t e[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) e[q] = d[q];
+        const int sh = 2 * (e0 & 1);
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(e[1], e[0], sh);
+        const uint32_t w1 = __builtin_amdgcn_alignbyte(e[2], e[1], sh);
+        const uint32_t w2 = __builtin_amdgcn_alignbyte(e[3], e[2], sh);
+        const uint32_t w3 = __builtin_amdgcn_alignbyte(e[4], e[3], sh);
+        bf[s][u][l] = __builtin_bit_cast(h8, uint4{w0, w1, w2, w3});
+      }
     }
   }
   // from here on the only vector-memory operations are the DMA pieces and the epilogue stores
 
+  constexpr int kSteady = (kRing - 2) * kMaxPerChunk + (kRing - 1) * kStoresPerChunk;
   for (int i = 0; i < n; ++i) {
     // Retire slot i: after its pieces this wave issued min(kRing-2, n-1-i) later chunks' pieces
     // and the stores of min(i, kRing-1) chunks (stores of chunk j follow the pieces of j+kRing-1).
     const int later = min(kRing - 2, n - 1 - i) * perChunk + min(i, kRing - 1) * kStoresPerChunk;
-    vmWaitDyn<0, (kRing - 2) * ((G::kPieces + kI8Waves - 1) / kI8Waves) + (kRing - 1) * kStoresPerChunk>(
-        waveUniform(later));
+    if (later == kSteady) vmWait<kSteady>();  // the steady state of the widest waves
+    else vmWaitDyn<0, kSteady>(waveUniform(later));
     ldsBarrier();  // every wave's pieces of slot i landed; compute(i-1) done with the planes
     const int slot = i % kRing;
-    splitSlot<S>(ring + slot * G::kSlot, planes, shift, tid);
+    splitSlot<S>(ring + kRingPad + slot * G::kSlot + sub, planes, sub, tid);
     if (a.carryDst != nullptr && G0 == 0 && i == 0) {
       // streaming history: the only block that reads samples [0, T - 1) has them in LDS now,
       // so the carry may overwrite them in place (source [nOut, nIn) is disjoint: nOut >= T - 1)
@@ -330,13 +359,13 @@ __global__ __launch_bounds__(kI8Threads, 3) void firI8MfmaKernel(I8FirArgs a) {
     }
     // refill the slot chunk i-1 used (its split finished before the barrier above)
     if (i + kRing - 1 < n)
-      issueChunk<S>(a, alignedBase, lastBlock, G0 + i + kRing - 1, ringLds + ((i + kRing - 1) % kRing) * G::kSlot,
+      issueChunk<S>(alignedBase, lastBlock, G0 + i + kRing - 1, ringLds + ((i + kRing - 1) % kRing) * G::kSlot,
                     wave, lane);
     ldsBarrier();  // planes complete
     const int64_t chunkOut = (int64_t)(G0 + i) * kI8ChunkOut;
 #pragma unroll
     for (int t = 0; t < kI8TilesPerWave; ++t)
-      computeTile<S, EPI>(a, planes, bf, chunkOut, wave * kI8TilesPerWave + t, lane, outScale, hiScale);
+      computeTile<S, EPI>(a, planes, bf, chunkOut, wave * kI8TilesPerWave + t, lane, outScale);
   }
   vmWait<0>();  // no DMA may still target this block's LDS when it exits
 }
@@ -353,7 +382,7 @@ hipError_t launchI8(const I8FirArgs& a, int epi, hipStream_t stream, int grid) {
 }  // namespace
 
 bool firI8MfmaEligible(size_t tapCount, size_t decimation, const void* in) {
-  // IQ samples are 2-byte pairs; any sample-aligned pointer works (the split pass re-aligns)
+  // IQ samples are 2-byte pairs; any sample-aligned pointer works (the DMA re-aligns)
   return tapCount >= 1 && tapCount <= 32 * kI8MaxS - 31 && decimation <= 1 &&
          (reinterpret_cast<uintptr_t>(in) & 1u) == 0;
 }
@@ -372,7 +401,7 @@ hipError_t launchFirI8Mfma(const int8_t* iq, const float* taps, size_t tapCount,
   const int64_t chunks = ((int64_t)nOut + kI8ChunkOut - 1) / kI8ChunkOut;
   if (chunks > 0x7fffffff) return hipErrorInvalidValue;
   a.chunks = (int32_t)chunks;
-  // 3 resident blocks per CU (<= 168 VGPRs, 46 KB LDS); each streams a contiguous chunk range
+  // 3 resident blocks per CU (<= 168 VGPRs); each streams a contiguous chunk range
   const int grid = (int)(chunks < 256 * 3 ? chunks : 256 * 3);
   const int S = (int)((tapCount + 31 + 31) / 32);
   switch (S) {

@@ -199,9 +199,11 @@ def test_int8_mfma_path(ops, orc, T, n_out):
     x = orc.int8_to_float(iq).view(np.complex64)
     y64, bound = orc.fir_f64(taps, x, 1, n_out)
     _check_fir(y, y64, bound, ("mfma", T, n_out))
-    # the MFMA epilogue takes the hardware square root (v_sqrt_f32, <= 1 ulp)
+    # the MFMA epilogue forms |y| from the unscaled accumulators with the hardware square root
+    # (v_sqrt_f32, <= 1 ulp) and scales once: a few ulp from AM of the rounded complex output
     am_ref = orc.quad_am_demod(y)
-    assert np.all(np.abs(am - am_ref) <= np.spacing(am_ref))
+    assert np.all(np.abs(am - am_ref) <= 4 * np.spacing(am_ref))
+    assert np.all(np.abs(am - np.abs(y64)) <= FIR_TOL * bound + 1e-30)
     prev = ops.set_kernel_policy(ops.POLICY_NO_MFMA)
     try:
         y_valu = _host(ops.fir(taps_d, iq_d, 1, n_out, int8_iq=True))
