@@ -47,10 +47,28 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr int kI8Waves = 4;
 constexpr int kI8Threads = kI8Waves * kWave;
 constexpr int kI8TileOut = 512;                                        // 16 rows x 32 columns
-constexpr int kI8TilesPerWave = 2;
+// Tuning knobs (tools/exp builds variants of this file with -D overrides; the product uses the
+// defaults).
+#ifndef GSDR_I8_TILES_PER_WAVE
+#define GSDR_I8_TILES_PER_WAVE 2
+#endif
+#ifndef GSDR_I8_RING
+#define GSDR_I8_RING 3
+#endif
+#ifndef GSDR_I8_BLOCKS_PER_CU
+#define GSDR_I8_BLOCKS_PER_CU 3
+#endif
+#ifndef GSDR_I8_EXPERIMENT
+#define GSDR_I8_EXPERIMENT 0  // attribution builds only: 1 = skip split, 2 = skip MFMA, 4 = skip epilogue,
+                              // 8 = no DMA (compute on stale LDS), 16 = no stores, 32 = clock stamps
+#endif
+#ifndef GSDR_I8_PIPE
+#define GSDR_I8_PIPE 0  // 1: a tile's MFMAs overlap the previous tile's epilogue (sched_group_barrier)
+#endif
+constexpr int kI8TilesPerWave = GSDR_I8_TILES_PER_WAVE;
 constexpr int kI8ChunkOut = kI8Waves * kI8TilesPerWave * kI8TileOut;  // 4096 outputs per chunk
 constexpr int kI8MaxS = 5;                                             // K <= 160 -> T <= 129
-constexpr int kRing = 3;                                               // LDS-DMA ring slots
+constexpr int kRing = GSDR_I8_RING;                                    // LDS-DMA ring slots
 constexpr int kPiece = 64 * 16;                                        // bytes per wave DMA instruction
 constexpr int kRingPad = 16;                                           // room for the DMA re-alignment
 // Epilogue stores per wave per chunk (one store instruction per lane output, 8 per tile).
@@ -245,33 +263,99 @@ __device__ __forceinline__ void tileEpilogue(const I8FirArgs& a, const v16f& acc
   }
 }
 
+// One software-pipeline stage of a wave: the MFMAs of `tile` into accNew with the epilogue of
+// the previous tile (accOld, outputs from oldOut) placed between them by hand: sched_barrier(0)
+// fences pin the order, so the vector ALU works while the matrix pipe runs (an MFMA holds the
+// SIMD's vector issue for only 8 of its 32 cycles).
+template <int S, int EPI>
+__device__ __forceinline__ void pipeStage(const I8FirArgs& a, const int8_t* planes, const h8 (&bf)[S][2][2],
+                                          int tile, v16f& accNew, const v16f& accOld, int64_t oldOut, bool haveOld,
+                                          int lane, float outScale) {
+  if (haveOld && oldOut + kI8TileOut <= a.nOut) {  // wave-uniform steady state
+    constexpr int kPlaneBytes = I8Geom<S>::kPlaneBytes;
+    const int row = lane & 31;
+    const int half = lane >> 5;
+    const int8_t* plane = planes + (row >> 4) * kPlaneBytes;
+    const int b0 = tile * 16 + (row & 15);
+    const int64_t rowOut = oldOut + 4 * half * 32 + (lane & 31);
+    auto frag = [&](int j) {  // K-half j = 2 s + u
+      return *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0 + (j >> 1), 2 * (j & 1) + half));
+    };
+    auto out = [&](int i) {  // epilogue of output register i of the old tile
+      const int64_t k = rowOut + 32 * ((i & 3) + 8 * (i >> 2));
+      if (EPI == kEpiAm) {
+        const float m2 = fmaf(accOld[i], accOld[i], accOld[i + 8] * accOld[i + 8]);
+        reinterpret_cast<float*>(a.out)[k] = __builtin_amdgcn_sqrtf(m2) * outScale;
+      } else {
+        reinterpret_cast<f2*>(a.out)[k] = f2{accOld[i], accOld[i + 8]} * outScale;
+      }
+    };
+    h8 f0 = frag(0), f1 = frag(1), f2v;
+    accNew = v16f{};
+#pragma unroll
+    for (int j = 0; j < 2 * S; ++j) {
+      if (j + 2 < 2 * S) f2v = frag(j + 2);
+      accNew = __builtin_amdgcn_mfma_f32_32x32x16_f16(f0, bf[j >> 1][j & 1][0], accNew, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (j < 8) out(j);
+      __builtin_amdgcn_sched_barrier(0);
+      accNew = __builtin_amdgcn_mfma_f32_32x32x16_f16(f0, bf[j >> 1][j & 1][1], accNew, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      f0 = f1;
+      f1 = f2v;
+    }
+  } else {
+    tileMfma<S>(planes, bf, tile, lane, accNew);
+    if (haveOld) tileEpilogue<EPI, false>(a, accOld, oldOut, lane, outScale);
+  }
+}
+
 template <int S, int EPI>
 __device__ __forceinline__ void computeTile(const I8FirArgs& a, const int8_t* planes, const h8 (&bf)[S][2][2],
                                             int64_t chunkOut, int tile, int lane, float outScale) {
   v16f acc;
-  tileMfma<S>(planes, bf, tile, lane, acc);
+  if (GSDR_I8_EXPERIMENT & 2) {
+    acc = v16f{} + (float)*reinterpret_cast<const _Float16*>(planes + 16 * lane);
+  } else {
+    tileMfma<S>(planes, bf, tile, lane, acc);
+  }
   const int64_t tileOut = chunkOut + (int64_t)tile * kI8TileOut;
+  if (GSDR_I8_EXPERIMENT & 16) {  // no stores at all (keeps the accumulator live)
+    if (acc[0] + acc[5] + acc[9] + acc[15] == 1.2345f) reinterpret_cast<float*>(a.out)[lane] = 0.0f;
+    return;
+  }
+  if (GSDR_I8_EXPERIMENT & 4) {
+    const int64_t rowOut = tileOut + 4 * (lane >> 5) * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (rowOut + 32 * ((i & 3) + 8 * (i >> 2)) < a.nOut)
+        reinterpret_cast<float*>(a.out)[rowOut + 32 * ((i & 3) + 8 * (i >> 2))] = acc[i];
+    return;
+  }
   if (tileOut + kI8TileOut <= a.nOut) tileEpilogue<EPI, true>(a, acc, tileOut, lane, outScale);
   else tileEpilogue<EPI, false>(a, acc, tileOut, lane, outScale);
 }
 
 template <int S, int EPI>
-__global__ __launch_bounds__(kI8Threads, 3) void firI8MfmaKernel(I8FirArgs a) {
+__global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKernel(I8FirArgs a) {
   using G = I8Geom<S>;
   __shared__ __attribute__((aligned(16))) int8_t ring[kRingPad + kRing * G::kSlot];
   __shared__ __attribute__((aligned(16))) int8_t planes[2 * G::kPlaneBytes];
   __shared__ __attribute__((aligned(16))) _Float16 limbTab[2 * kLimbRow];
   __shared__ float waveMax[kI8Waves];
 
+  const uint64_t tStart = (GSDR_I8_EXPERIMENT & 32) ? __builtin_amdgcn_s_memrealtime() : 0;
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wave = waveUniform(tid >> 6);
   const int T = a.T;
 
   // this block's contiguous chunk range
-  const int G0 = (int)(((int64_t)blockIdx.x * a.chunks) / gridDim.x);
-  const int G1 = (int)(((int64_t)(blockIdx.x + 1) * a.chunks) / gridDim.x);
-  const int n = G1 - G0;
+  // (q chunks each, one more for the first r blocks: with blocks b, b + 256, b + 512 sharing a CU
+  // under round-robin dispatch, the surplus spreads one per CU first - a speed heuristic only)
+  const int q = a.chunks / (int)gridDim.x, r = a.chunks % (int)gridDim.x;
+  const int G0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
+  const int n = q + ((int)blockIdx.x < r ? 1 : 0);
   if (n <= 0) return;  // block-uniform, before any barrier or DMA
 
   // ---- tap load, then the ring prologue (chunks 0 .. kRing-2 of the range) -------------------
@@ -292,7 +376,8 @@ __global__ __launch_bounds__(kI8Threads, 3) void firI8MfmaKernel(I8FirArgs a) {
   constexpr int kMaxPerChunk = (G::kPieces + kI8Waves - 1) / kI8Waves;
 #pragma unroll
   for (int j = 0; j < kRing - 1; ++j)
-    if (j < n) issueChunk<S>(alignedBase, lastBlock, G0 + j, ringLds + j * G::kSlot, wave, lane);
+    if (j < n && !(GSDR_I8_EXPERIMENT & 8))
+      issueChunk<S>(alignedBase, lastBlock, G0 + j, ringLds + j * G::kSlot, wave, lane);
   reinterpret_cast<uint32_t*>(limbTab)[tid] = 0u;  // 2 rows x 256 f16 = one dword per thread
   vmWaitDyn<0, (kRing - 1) * kMaxPerChunk>(waveUniform(min(kRing - 1, n) * perChunk));
   asm volatile("" : "+v"(hv));  // hv is defined only after the wait
@@ -342,15 +427,25 @@ __global__ __launch_bounds__(kI8Threads, 3) void firI8MfmaKernel(I8FirArgs a) {
   // from here on the only vector-memory operations are the DMA pieces and the epilogue stores
 
   constexpr int kSteady = (kRing - 2) * kMaxPerChunk + (kRing - 1) * kStoresPerChunk;
+  uint64_t t0c = 0, t0r = 0;
+  if (GSDR_I8_EXPERIMENT & 32) {
+    t0c = __builtin_amdgcn_s_memtime();
+    t0r = __builtin_amdgcn_s_memrealtime();
+  }
+  (void)tStart;
+  v16f accPrev = v16f{};
+  int64_t prevOut = 0;
   for (int i = 0; i < n; ++i) {
     // Retire slot i: after its pieces this wave issued min(kRing-2, n-1-i) later chunks' pieces
     // and the stores of min(i, kRing-1) chunks (stores of chunk j follow the pieces of j+kRing-1).
-    const int later = min(kRing - 2, n - 1 - i) * perChunk + min(i, kRing - 1) * kStoresPerChunk;
-    if (later == kSteady) vmWait<kSteady>();  // the steady state of the widest waves
+    const int later = min(kRing - 2, n - 1 - i) * perChunk + min(i, kRing - 1) * kStoresPerChunk -
+                      ((GSDR_I8_PIPE && i > 0 && i <= kRing - 1) ? kStoresPerChunk / 2 : 0);
+    if (GSDR_I8_EXPERIMENT & 8) {
+    } else if (later == kSteady) vmWait<kSteady>();  // the steady state of the widest waves
     else vmWaitDyn<0, kSteady>(waveUniform(later));
     ldsBarrier();  // every wave's pieces of slot i landed; compute(i-1) done with the planes
     const int slot = i % kRing;
-    splitSlot<S>(ring + kRingPad + slot * G::kSlot + sub, planes, sub, tid);
+    if (!(GSDR_I8_EXPERIMENT & 1)) splitSlot<S>(ring + kRingPad + slot * G::kSlot + sub, planes, sub, tid);
     if (a.carryDst != nullptr && G0 == 0 && i == 0) {
       // streaming history: the only block that reads samples [0, T - 1) has them in LDS now,
       // so the carry may overwrite them in place (source [nOut, nIn) is disjoint: nOut >= T - 1)
@@ -358,16 +453,38 @@ __global__ __launch_bounds__(kI8Threads, 3) void firI8MfmaKernel(I8FirArgs a) {
       for (int t = tid; t < T - 1; t += kI8Threads) reinterpret_cast<uint16_t*>(a.carryDst)[t] = src[t];
     }
     // refill the slot chunk i-1 used (its split finished before the barrier above)
-    if (i + kRing - 1 < n)
+    if (i + kRing - 1 < n && !(GSDR_I8_EXPERIMENT & 8))
       issueChunk<S>(alignedBase, lastBlock, G0 + i + kRing - 1, ringLds + ((i + kRing - 1) % kRing) * G::kSlot,
                     wave, lane);
     ldsBarrier();  // planes complete
     const int64_t chunkOut = (int64_t)(G0 + i) * kI8ChunkOut;
+    if constexpr (GSDR_I8_PIPE) {
+      static_assert(!GSDR_I8_PIPE || kI8TilesPerWave == 2, "the pipelined path pairs two tiles per wave");
+      const int t0 = 2 * wave;
+      v16f accA, accB;
+      pipeStage<S, EPI>(a, planes, bf, t0, accA, accPrev, prevOut, i > 0, lane, outScale);
+      pipeStage<S, EPI>(a, planes, bf, t0 + 1, accB, accA, chunkOut + (int64_t)t0 * kI8TileOut, true, lane,
+                        outScale);
+      accPrev = accB;
+      prevOut = chunkOut + (int64_t)(t0 + 1) * kI8TileOut;
+    } else {
 #pragma unroll
-    for (int t = 0; t < kI8TilesPerWave; ++t)
-      computeTile<S, EPI>(a, planes, bf, chunkOut, wave * kI8TilesPerWave + t, lane, outScale);
+      for (int t = 0; t < kI8TilesPerWave; ++t)
+        computeTile<S, EPI>(a, planes, bf, chunkOut, wave * kI8TilesPerWave + t, lane, outScale);
+    }
   }
+  if constexpr (GSDR_I8_PIPE) tileEpilogue<EPI, false>(a, accPrev, prevOut, lane, outScale);
   vmWait<0>();  // no DMA may still target this block's LDS when it exits
+  if ((GSDR_I8_EXPERIMENT & 32) && tid == 0) {
+    const uint64_t tc = __builtin_amdgcn_s_memtime(), tr = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    uint32_t* st = reinterpret_cast<uint32_t*>(a.out) + 4 * blockIdx.x;
+    st[0] = (uint32_t)(tc - t0c);
+    st[1] = (uint32_t)(tr - t0r);
+    st[2] = (uint32_t)tStart;
+    st[3] = (uint32_t)t0r;
+    reinterpret_cast<uint32_t*>(a.out)[4 * 768 + blockIdx.x] = (uint32_t)tr;
+  }
 }
 
 namespace {
@@ -402,7 +519,7 @@ hipError_t launchFirI8Mfma(const int8_t* iq, const float* taps, size_t tapCount,
   if (chunks > 0x7fffffff) return hipErrorInvalidValue;
   a.chunks = (int32_t)chunks;
   // 3 resident blocks per CU (<= 168 VGPRs); each streams a contiguous chunk range
-  const int grid = (int)(chunks < 256 * 3 ? chunks : 256 * 3);
+  const int grid = (int)(chunks < 256 * GSDR_I8_BLOCKS_PER_CU ? chunks : 256 * GSDR_I8_BLOCKS_PER_CU);
   const int S = (int)((tapCount + 31 + 31) / 32);
   switch (S) {
     case 1: return launchI8<1>(a, epi, stream, grid);
