@@ -42,7 +42,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "Msamples/sec through FIR→QuadAmDemod chain at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, spec
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md, FP32 vector (packed FMA)
-INT8_PEAK_TOPS = 5000.0        # MI355X_MICROARCH.md, I8 MFMA dense (2x the BF16 rate)
+F16_PEAK_TFLOPS = 2500.0       # MI355X_MICROARCH.md, BF16/F16 MFMA dense
 
 WORKLOADS = {
     # name: (description, input kind, samples per GPU step, taps, decimation, cutoff, window, fs)
@@ -146,14 +146,14 @@ class ShardedChain:
 
     def timed_bytes_ops(self):
         """Algorithmic bytes of the timed launch (input read once + output written once) and
-        its arithmetic: int8 MFMA ops for the exact int8 kernel, direct-form FMA flops else."""
+        its arithmetic: f16 MFMA flops for the int8 IQ MFMA kernel, direct-form FMA flops else."""
         g = self.geom
         n = g.outputs if self.single else g.outputs - g.head_outputs
         n_in = (n - 1) * self.D + self.T
         in_bytes = n_in * (2 if self.kind == "i8" else 8)
         if self.mfma_int8:
-            s = (self.T + 62) // 32  # K-steps of 32: K = 32 S >= T + 31
-            return in_bytes + n * 4, n * 2 * 4 * 32 * s * 2  # I and Q rows x 4 limbs x K MACs x 2
+            s = (self.T + 62) // 32  # K-blocks of 32: K = 32 S >= T + 31
+            return in_bytes + n * 4, n * 2 * 2 * 32 * s * 2  # I and Q rows x 2 f16 limbs x K MACs x 2
         return in_bytes + n * 4, n * self.T * 4
 
     @property
@@ -296,9 +296,9 @@ def main():
                 "traffic": traffic,
                 "avg_launch_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": bytes_,
-                "compute": ({"kind": "int8 MFMA (4 tap limbs)", "achieved_tops": achieved_t,
-                             "peak_tops": INT8_PEAK_TOPS, "frac": achieved_t / INT8_PEAK_TOPS,
-                             "ops_per_launch": ops_} if chain.mfma_int8 else
+                "compute": ({"kind": "f16 MFMA (2 tap limbs, fp32 accumulate)", "achieved_tflops": achieved_t,
+                             "peak_tflops": F16_PEAK_TFLOPS, "frac": achieved_t / F16_PEAK_TFLOPS,
+                             "flops_per_launch": ops_} if chain.mfma_int8 else
                             {"kind": "fp32 VALU FMA", "achieved_tflops": achieved_t,
                              "peak_tflops": FP32_PEAK_TFLOPS, "frac": achieved_t / FP32_PEAK_TFLOPS,
                              "flops_per_launch": ops_}),
