@@ -434,6 +434,11 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
     if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firI8MfmaEligible(tapCount, decimation, in))
       return launchFirI8Mfma(static_cast<const int8_t*>(in), taps, tapCount, out, nOut, EPI, stream);
   }
+  // cf32 with real taps: the split-precision bf16 MFMA kernel for the long-filter shapes
+  if constexpr (MODE == kFirFC && INK == kInCF32 && EPI != kEpiPair) {
+    if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firCfMfmaEligible(tapCount, decimation, in))
+      return launchFirCfMfma(static_cast<const float*>(in), taps, tapCount, decimation, out, nOut, EPI, stream);
+  }
 
   const FirPlanShape s = planFirShape(tapCount, decimation);
   FirArgs a{};

@@ -1,0 +1,387 @@
+// MFMA FIR for cf32 input and real taps (gsdrFirFC / gsdrFirFCAmDemod: the C3 / C4 chains, up to
+// K = 31 D + T <= 1408, D <= 16), split-precision bf16 on v_mfma_f32_32x32x16_bf16.
+//
+// Arithmetic. Every fp32 value v (sample component or tap) is split EXACTLY into three bf16
+// limbs by round-to-nearest: v0 = bf16(v), v1 = bf16(v - v0), v2 = v - v0 - v1 (<= 8 significant
+// bits, exact in bf16), |v1| <= 2^-9 |v|, |v2| <= 2^-18 |v|. The kernel sums the six products
+// x_i h_j with i + j <= 2; the dropped ones are below 2^-26 |x h|. The MFMA forms each bf16
+// product exactly and accumulates in fp32, so the result carries the rounding of an fp32
+// accumulation - the class of the reference's fp32 direct form (tests: 1e-6 of sum |h||x|).
+//
+// GEMM shape (decimating Toeplitz). Output k = 32 m + n of a 512-output tile (m < 16 rows,
+// n < 32 columns):
+//     C[m][n] = sum_kappa A[m][kappa] B[kappa][n],  A[m][kappa] = x[32 D m + kappa],
+//     B[kappa][n] = h[kappa - n D] (0 <= kappa - n D < T, else 0),  kappa < K = 31 D + T.
+// A rows 0-15 read the I planes, rows 16-31 the Q planes of the same 16 output rows, so a lane
+// holds I and Q of one output in accumulator registers i and i + 8.
+//
+// Work split. One 512-thread block per CU walks a contiguous range of tiles. The tile's input
+// window (W = 480 D + 128 KS samples) is loaded into registers one tile ahead, split into six
+// bf16 planes (3 limbs x I/Q) in LDS, and the K range is split over the 8 waves (KS K-steps of 16
+// each): a wave's B fragments (3 limbs x KS K-steps of the Toeplitz tap matrix) stay in VGPRs for
+// the whole launch. Partial accumulators meet in LDS; each wave reduces and stores 64 outputs.
+// Plane units (8 samples, 16 B) are padded (unit u at u + (u >> padShift)) and the I / Q planes
+// offset so that every ds_read_b128 lane group of the A fragments is bank-conflict free; the host
+// picks both per D (cfPlaneLayout).
+#include <mutex>
+
+#include "kcommon.h"
+#include "fir_launch.h"
+
+namespace gsdr_amd {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+constexpr int kCfWaves = 8;
+constexpr int kCfThreads = kCfWaves * kWave;
+constexpr int kCfTileOut = 512;  // 16 rows x 32 columns
+constexpr int kCfMaxKS = 11;     // K-steps of 16 per wave: K <= 8 x 11 x 16 = 1408
+constexpr int kCfMaxD = 16;
+constexpr int kCfPartialBytes = kCfWaves * 16 * kWave * 4;  // 32 KB
+constexpr int kCfDynLdsMax = 160 * 1024 - 256;             // the rest: static flags
+
+struct CfFirArgs {
+  const float* x;     // interleaved re, im
+  const float* taps;
+  void* out;
+  int64_t nOut;
+  int64_t nIn;        // complex samples readable: (nOut - 1) D + T
+  int32_t T;
+  int32_t D;
+  int32_t KS;         // K-steps per wave
+  int32_t tiles;
+  int32_t Wu;         // window units (8 samples) per tile = 60 D + 16 KS
+  int32_t padShift;   // plane unit u lives at u + (u >> padShift)
+  int32_t planeStride;  // bytes between the six planes (limb l, component c at 2 l + c)
+};
+
+__device__ __forceinline__ int cfPhys(int u, int p) { return u + (u >> p); }
+
+// fp32 pair -> three bf16 limb pairs (exact).
+__device__ __forceinline__ void split3(float a, float b, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  const f2v v = {a, b};
+  const bf2 h0 = __builtin_convertvector(v, bf2);
+  const f2v r1 = v - __builtin_convertvector(h0, f2v);
+  const bf2 h1 = __builtin_convertvector(r1, bf2);
+  const f2v r2 = r1 - __builtin_convertvector(h1, f2v);
+  const bf2 h2 = __builtin_convertvector(r2, bf2);
+  l0 = __builtin_bit_cast(uint32_t, h0);
+  l1 = __builtin_bit_cast(uint32_t, h1);
+  l2 = __builtin_bit_cast(uint32_t, h2);
+}
+
+// Window loads: G groups of 8 samples (64 B) per thread, group g = tid + 512 j.
+template <int G>
+struct CfWindow {
+  f4 v[G][4];  // native vector type: HIP's float4 union defeats register promotion
+};
+
+template <int G>
+__device__ __forceinline__ void loadWindow(const CfFirArgs& a, int tile, int tid, CfWindow<G>& w) {
+  const int64_t s0 = (int64_t)tile * kCfTileOut * a.D;
+  const bool inside = s0 + 8 * (int64_t)a.Wu <= a.nIn;  // block-uniform
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int g = tid + kCfThreads * j;
+    const int64_t smp = s0 + 8 * (int64_t)g;
+    if (g < a.Wu) {
+      if (inside) {
+        const f4* p = reinterpret_cast<const f4*>(a.x + 2 * smp);  // 16-byte aligned base
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w.v[j][q] = p[q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t i0 = smp + 2 * q;
+          const f2 e0 = i0 < a.nIn ? reinterpret_cast<const f2*>(a.x)[i0] : f2{0.f, 0.f};
+          const f2 e1 = i0 + 1 < a.nIn ? reinterpret_cast<const f2*>(a.x)[i0 + 1] : f2{0.f, 0.f};
+          w.v[j][q] = f4{e0.x, e0.y, e1.x, e1.y};
+        }
+      }
+    }
+  }
+}
+
+// Split the window into the planes; a non-finite sample sets *nonFinite (0 * x is NaN exactly
+// for x = +-inf or NaN), so the tile takes the direct path: the Toeplitz product would multiply
+// the sample by the zero taps of outputs whose windows do not contain it (0 * inf = NaN).
+template <int G>
+__device__ __forceinline__ void splitWindow(const CfFirArgs& a, const CfWindow<G>& w, int8_t* planes, int tid,
+                                            int* nonFinite) {
+  f4 probe = f4{};
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int g = tid + kCfThreads * j;
+    if (g < a.Wu) {
+      uint32_t iL[3][4], qL[3][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // samples 2q, 2q + 1: (re, im, re, im)
+        split3(w.v[j][q].x, w.v[j][q].z, iL[0][q], iL[1][q], iL[2][q]);
+        split3(w.v[j][q].y, w.v[j][q].w, qL[0][q], qL[1][q], qL[2][q]);
+        probe += w.v[j][q] * 0.0f;
+      }
+      const int off = 16 * cfPhys(g, a.padShift);
+#pragma unroll
+      for (int l = 0; l < 3; ++l) {
+        *reinterpret_cast<uint4*>(planes + (2 * l) * a.planeStride + off) = uint4{iL[l][0], iL[l][1], iL[l][2], iL[l][3]};
+        *reinterpret_cast<uint4*>(planes + (2 * l + 1) * a.planeStride + off) =
+            uint4{qL[l][0], qL[l][1], qL[l][2], qL[l][3]};
+      }
+    }
+  }
+  const float pr = (probe.x + probe.y) + (probe.z + probe.w);
+  if (pr != pr) *nonFinite = 1;
+}
+
+// Direct fp32 form of one tile, one output per thread (tiles holding a non-finite sample).
+template <int EPI>
+__device__ __forceinline__ void directTile(const CfFirArgs& a, int tile, int tid) {
+  const int64_t k = (int64_t)tile * kCfTileOut + tid;
+  if (k >= a.nOut) return;
+  const f2* x = reinterpret_cast<const f2*>(a.x) + k * a.D;
+  f2 y = f2{0.0f, 0.0f};
+  for (int j = 0; j < a.T; ++j) y += a.taps[j] * x[j];
+  if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(y);
+  else reinterpret_cast<f2*>(a.out)[k] = y;
+}
+
+template <int G, int EPI>
+__global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  int8_t* planes = smem;
+  float* part = reinterpret_cast<float*>(smem + 6 * a.planeStride);
+  __shared__ int nonFinite[2];  // per tile parity: the window holds an inf / NaN
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int D = a.D, T = a.T, KS = a.KS;
+
+  // contiguous tile range of this block
+  const int q = a.tiles / (int)gridDim.x, r = a.tiles % (int)gridDim.x;
+  const int t0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
+  const int n = q + ((int)blockIdx.x < r ? 1 : 0);
+  if (n <= 0) return;
+
+  // first window in flight while the taps are prepared
+  CfWindow<G> win;
+  loadWindow<G>(a, t0, tid, win);
+
+  // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), then this wave's B fragments -------------
+  if (tid < 2) nonFinite[tid] = 0;
+  const int off0 = 31 * D;
+  const int span = off0 + 128 * KS;
+  for (int i = tid; i < span; i += kCfThreads) {
+    const int j = i - off0;
+    part[i] = (j >= 0 && j < T) ? a.taps[j] : 0.0f;
+  }
+  __syncthreads();
+  const int half = lane >> 5;
+  const int col = lane & 31;
+  bf8 bf[kCfMaxKS][3];
+#pragma unroll
+  for (int s = 0; s < kCfMaxKS; ++s) {
+    if (s < KS) {
+      const int kap = 16 * (wave * KS + s) + 8 * half;  // first kappa of this lane's 8
+      uint32_t l[3][4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float h0 = part[off0 + kap + 2 * p - col * D];
+        const float h1 = part[off0 + kap + 2 * p + 1 - col * D];
+        split3(h0, h1, l[0][p], l[1][p], l[2][p]);
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) bf[s][i] = __builtin_bit_cast(bf8, uint4{l[i][0], l[i][1], l[i][2], l[i][3]});
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) bf[s][i] = bf8{};
+    }
+  }
+  __syncthreads();  // the tap staging area becomes the partial-sum area
+
+  // ---- prologue: tile t0's window into the planes, tile t0 + 1's loads in flight -------------
+  splitWindow<G>(a, win, planes, tid, &nonFinite[t0 & 1]);
+  if (n > 1) loadWindow<G>(a, t0 + 1, tid, win);
+  __syncthreads();
+
+  // A-fragment geometry: row r = lane & 15 of component c = (lane >> 4) & 1, K-half `half`
+  const int arow = lane & 15;
+  const int comp = (lane >> 4) & 1;
+  const int uRow = 4 * D * arow + half;
+  const int8_t* pI = planes + comp * a.planeStride;
+
+  for (int i = 0; i < n; ++i) {
+    const int tile = t0 + i;
+    const bool direct = nonFinite[tile & 1] != 0;  // block-uniform (set before the last barrier)
+    if (tid == 0) nonFinite[(tile + 1) & 1] = 0;    // last read in tile - 1's compute
+    if (direct) {
+      directTile<EPI>(a, tile, tid);
+      __syncthreads();  // the flag reset above precedes the next split's writes
+    } else {
+    // ---- this wave's K range: KS K-steps x 6 split-precision MFMAs ---------------------------
+    v16f acc = v16f{};
+#pragma unroll
+    for (int s = 0; s < kCfMaxKS; ++s) {
+      if (s < KS) {
+        const int u = uRow + 2 * (wave * KS + s);
+        const int off = 16 * cfPhys(u, a.padShift);
+        const bf8 x0 = *reinterpret_cast<const bf8*>(pI + off);
+        const bf8 x1 = *reinterpret_cast<const bf8*>(pI + 2 * a.planeStride + off);
+        const bf8 x2 = *reinterpret_cast<const bf8*>(pI + 4 * a.planeStride + off);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x0, bf[s][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x0, bf[s][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, bf[s][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x0, bf[s][2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, bf[s][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, bf[s][0], acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
+    __syncthreads();  // partials complete; every wave is done reading the planes
+
+    // ---- reduction + epilogue: wave w finishes accumulator register w (I) / w + 8 (Q) --------
+    float yi = 0.0f, yq = 0.0f;
+#pragma unroll
+    for (int v = 0; v < kCfWaves; ++v) {
+      yi += part[(v * 16 + wave) * kWave + lane];
+      yq += part[(v * 16 + wave + 8) * kWave + lane];
+    }
+    const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * half;
+    const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
+    if (k < a.nOut) {
+      if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq});
+      else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq};
+    }
+    }
+
+    // ---- next tile's window into the planes, the one after into registers ------------------
+    if (i + 1 < n) {
+      splitWindow<G>(a, win, planes, tid, &nonFinite[(tile + 1) & 1]);
+      if (i + 2 < n) loadWindow<G>(a, tile + 2, tid, win);
+      __syncthreads();
+    }
+  }
+}
+
+// ---- host side ------------------------------------------------------------------------------
+
+namespace {
+
+// Lane groups of ds_read_b128 (MI355X_MICROARCH.md, LDS): 4 x 16 lanes, one LDS cycle each.
+constexpr int kB128Groups[4][16] = {
+    {0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+    {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+    {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+    {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+
+struct CfLayout {
+  int padShift;
+  int planeStride;
+};
+
+// Pick the plane padding and the I/Q plane offset that minimise the A-fragment bank conflicts
+// for this (D, KS), within the LDS budget.
+CfLayout cfPlaneLayout(int D, int KS, int Wu) {
+  CfLayout best{4, 0};
+  double bestCost = 1e30;
+  for (int p = 4; p >= 1; --p) {
+    const int units = Wu + (Wu >> p) + 1;
+    const int base = (16 * units + 255) / 256 * 256;
+    for (int qoff = 0; qoff < 16; ++qoff) {
+      const int stride = base + 16 * qoff;
+      if (6 * stride + kCfPartialBytes > kCfDynLdsMax) continue;
+      double cost = 0;
+      for (int s = 0; s < kCfWaves * KS; ++s) {
+        for (const auto& grp : kB128Groups) {
+          int slots[16][4];
+          int cnt[16] = {};
+          int worst = 1;
+          for (int li = 0; li < 16; ++li) {
+            const int l = grp[li];
+            const int u = 4 * D * (l & 15) + 2 * s + (l >> 5);
+            const int unit = u + (u >> p) + (((l >> 4) & 1) ? stride / 16 : 0);
+            const int slot = unit & 15;
+            bool dup = false;
+            for (int c = 0; c < cnt[slot]; ++c) dup |= slots[slot][c] == unit;
+            if (!dup && cnt[slot] < 4) slots[slot][cnt[slot]++] = unit;
+            worst = cnt[slot] > worst ? cnt[slot] : worst;
+          }
+          cost += worst;
+        }
+      }
+      cost += 1e-3 * (6.0 * stride) / 1024.0;  // tie-break: less LDS
+      if (cost < bestCost) {
+        bestCost = cost;
+        best = CfLayout{p, stride};
+      }
+    }
+  }
+  return best;
+}
+
+template <int G, int EPI>
+hipError_t launchCfG(const CfFirArgs& a, size_t lds, int grid, hipStream_t stream) {
+  static std::once_flag once;
+  static hipError_t attrErr = hipSuccess;
+  std::call_once(once, [] {
+    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(&firCfMfmaKernel<G, EPI>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kCfDynLdsMax);
+  });
+  if (attrErr != hipSuccess) return attrErr;
+  hipLaunchKernelGGL((firCfMfmaKernel<G, EPI>), dim3(grid), dim3(kCfThreads), lds, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool firCfMfmaEligible(size_t tapCount, size_t decimation, const void* in) {
+  const size_t d = decimation < 1 ? 1 : decimation;
+  return tapCount >= 64 && d <= (size_t)kCfMaxD && 31 * d + tapCount <= (size_t)(kCfWaves * kCfMaxKS * 16) &&
+         (reinterpret_cast<uintptr_t>(in) & 15u) == 0;
+}
+
+hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, size_t decimation, void* out,
+                           size_t nOut, int epi, hipStream_t stream) {
+  CfFirArgs a{};
+  a.x = x;
+  a.taps = taps;
+  a.out = out;
+  a.D = (int32_t)(decimation < 1 ? 1 : decimation);
+  a.T = (int32_t)tapCount;
+  a.nOut = (int64_t)nOut;
+  a.nIn = (int64_t)(nOut - 1) * a.D + (int64_t)tapCount;
+  const int ksteps = (31 * a.D + a.T + 15) / 16;
+  a.KS = (ksteps + kCfWaves - 1) / kCfWaves;
+  const int64_t tiles = ((int64_t)nOut + kCfTileOut - 1) / kCfTileOut;
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  a.tiles = (int32_t)tiles;
+  a.Wu = 60 * a.D + 16 * a.KS;
+  static std::mutex mu;
+  static int cachedD = -1, cachedKS = -1;
+  static CfLayout cached{};
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    if (cachedD != a.D || cachedKS != a.KS) {
+      cached = cfPlaneLayout(a.D, a.KS, a.Wu);
+      cachedD = a.D;
+      cachedKS = a.KS;
+    }
+    a.padShift = cached.padShift;
+    a.planeStride = cached.planeStride;
+  }
+  const size_t lds = 6 * (size_t)a.planeStride + kCfPartialBytes;
+  if (a.planeStride == 0 || lds > (size_t)kCfDynLdsMax) return hipErrorInvalidValue;
+  const int grid = (int)(tiles < 256 ? tiles : 256);
+  const int G = (a.Wu + kCfThreads - 1) / kCfThreads;
+  switch (G) {
+    case 1: return epi == kEpiAm ? launchCfG<1, kEpiAm>(a, lds, grid, stream) : launchCfG<1, kEpiComplex>(a, lds, grid, stream);
+    case 2: return epi == kEpiAm ? launchCfG<2, kEpiAm>(a, lds, grid, stream) : launchCfG<2, kEpiComplex>(a, lds, grid, stream);
+    default: return epi == kEpiAm ? launchCfG<3, kEpiAm>(a, lds, grid, stream) : launchCfG<3, kEpiComplex>(a, lds, grid, stream);
+  }
+}
+
+}  // namespace gsdr_amd

@@ -36,6 +36,11 @@ bool firI8MfmaEligible(size_t tapCount, size_t decimation, const void* in);
 hipError_t launchFirI8Mfma(const int8_t* iq, const float* taps, size_t tapCount, void* out, size_t nOut, int epi,
                            hipStream_t stream, int8_t* carryDst = nullptr);
 
+// cf32 input x real taps -> FC FIR on split-precision bf16 MFMA (fir_cf_mfma.hip).
+bool firCfMfmaEligible(size_t tapCount, size_t decimation, const void* in);
+hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, size_t decimation, void* out,
+                           size_t nOut, int epi, hipStream_t stream);
+
 // Kernel-selection policy bits (gsdrAmdSetKernelPolicy).
 uint32_t kernelPolicy();
 
