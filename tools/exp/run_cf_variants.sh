@@ -1,0 +1,31 @@
+#!/bin/bash
+# Build and time variants of csrc/kernels/fir_cf_mfma.hip (same scheme as run_i8_variants.sh).
+set -eu
+cd "$(dirname "$0")/../.."
+OUT=tools/exp/_build_cf
+KSRC=cuda-sdr_amd/csrc/kernels/fir_cf_mfma.hip
+VARIANTS=${VARIANTS:-"base|
+nosplit|-DGSDR_CF_EXPERIMENT=1
+nomfma|-DGSDR_CF_EXPERIMENT=2
+noload|-DGSDR_CF_EXPERIMENT=4
+noreduce|-DGSDR_CF_EXPERIMENT=8
+mfma_only|-DGSDR_CF_EXPERIMENT=13
+split_only|-DGSDR_CF_EXPERIMENT=10"}
+if [ "${1:-build}" = build ]; then
+  mkdir -p $OUT
+  decls=""; table=""; objs=""; i=0
+  while IFS='|' read -r name flags; do
+    [ -z "$name" ] && continue
+    hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Iinclude -Icuda-sdr_amd/csrc/kernels -mllvm -amdgpu-mfma-vgpr-form \
+      -Dgsdr_amd=c$i $flags -c $KSRC -o $OUT/c$i.o &
+    decls="$decls DECL($i)"; table="$table {\"$name\", c$i::launchFirCfMfma},"; objs="$objs $OUT/c$i.o"
+    i=$((i+1))
+  done <<< "$VARIANTS"
+  wait
+  sed "s/namespace v##N/namespace c##N/" tools/exp/cf_bench.cpp > $OUT/cf_bench.cpp
+  hipcc --offload-arch=gfx950 -O2 -std=c++20 "-DVARIANT_DECLS=$decls" "-DVARIANT_TABLE=$table" -c $OUT/cf_bench.cpp -o $OUT/main.o
+  hipcc --offload-arch=gfx950 $OUT/main.o $objs -o $OUT/cf_bench
+  echo built $OUT/cf_bench
+else
+  timeout -k 10 300 $OUT/cf_bench
+fi
