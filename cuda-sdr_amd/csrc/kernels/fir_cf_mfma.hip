@@ -1,5 +1,5 @@
 // MFMA FIR for cf32 input and real taps (gsdrFirFC / gsdrFirFCAmDemod: the C3 / C4 chains, up to
-// K = 15 D + T <= 1536), split-precision bf16 on v_mfma_f32_16x16x32_bf16.
+// K = 31 D + T <= 1408, D <= 16), split-precision bf16 on v_mfma_f32_32x32x16_bf16.
 //
 // Arithmetic. Every fp32 value v (sample component or tap) is split EXACTLY into three bf16
 // limbs by round-to-nearest: v0 = bf16(v), v1 = bf16(v - v0), v2 = v - v0 - v1 (<= 8 significant
@@ -8,63 +8,60 @@
 // product exactly and accumulates in fp32, so the result carries the rounding of an fp32
 // accumulation - the class of the reference's fp32 direct form (tests: 1e-6 of sum |h||x|).
 //
-// GEMM shape (decimating Toeplitz). Output k = 16 m + n of a row block (m < 8 output rows,
-// n < 16 columns):
-//     C[m][n] = sum_kappa A[m][kappa] B[kappa][n],  A[m][kappa] = x[16 D m + kappa],
-//     B[kappa][n] = h[kappa - n D] (0 <= kappa - n D < T, else 0),  kappa < K = 15 D + T.
-// A rows 0-7 take the re parts, rows 8-15 the im parts of the same 8 output rows. A tile is two
-// row blocks (256 outputs).
+// GEMM shape (decimating Toeplitz). Output k = 32 m + n of a 512-output tile (m < 16 rows,
+// n < 32 columns):
+//     C[m][n] = sum_kappa A[m][kappa] B[kappa][n],  A[m][kappa] = x[32 D m + kappa],
+//     B[kappa][n] = h[kappa - n D] (0 <= kappa - n D < T, else 0),  kappa < K = 31 D + T.
+// A rows 0-15 read the I planes, rows 16-31 the Q planes of the same 16 output rows, so a lane
+// holds I and Q of one output in accumulator registers i and i + 8.
 //
-// Work split. One 512-thread block per CU walks a contiguous range of tiles. The K range is split
-// over the 8 waves (KS K-steps of 32 each): a wave's B fragments (3 limbs x KS K-steps of the
-// Toeplitz tap matrix) stay in VGPRs for the whole launch. The tile's input window (W = 240 D +
-// 256 KS samples) is loaded into registers two tiles ahead and split into six bf16 planes (3
-// limbs x re/im) in one of two LDS buffers one tile ahead, so a tile's split and its MFMAs use
-// different buffers: waves 0-3 split before their MFMAs, waves 4-7 after, and the two waves that
-// share a SIMD overlap the vector work of one with the matrix work of the other. One barrier per
-// tile; partial accumulators meet in (double-buffered) LDS and 256 threads reduce one output each.
-// The plane layout (padding, re/im plane offset) is picked per D against bank conflicts.
-//
-// Non-finite samples: the Toeplitz product multiplies a sample by the zero taps of outputs whose
-// windows do not contain it (0 * inf = NaN). A tile whose reduced outputs are not all finite is
-// recomputed in the direct fp32 form by the same threads (reference semantics).
+// Work split. One 512-thread block per CU walks a contiguous range of tiles. The tile's input
+// window (W = 480 D + 128 KS samples) is loaded into registers one tile ahead, split into six
+// bf16 planes (3 limbs x I/Q) in LDS, and the K range is split over the 8 waves (KS K-steps of 16
+// each): a wave's B fragments (3 limbs x KS K-steps of the Toeplitz tap matrix) stay in VGPRs for
+// the whole launch. Partial accumulators meet in LDS; each wave reduces and stores 64 outputs.
+// Plane units (8 samples, 16 B) are padded (unit u at u + (u >> padShift)) and the I / Q planes
+// offset so that every ds_read_b128 lane group of the A fragments is bank-conflict free; the host
+// picks both per D (cfPlaneLayout).
 #include <mutex>
 
 #include "kcommon.h"
 #include "fir_launch.h"
 
-#ifndef GSDR_CF_EXPERIMENT
-#define GSDR_CF_EXPERIMENT 0  // attribution builds only (tools/exp): 1 = skip split, 2 = skip MFMA,
-                              // 4 = skip loads
-#endif
-
 namespace gsdr_amd {
 
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 
+#ifndef GSDR_CF_EXPERIMENT
+#define GSDR_CF_EXPERIMENT 0  // attribution builds only (tools/exp): 1 = skip split, 2 = skip MFMA,
+                              // 4 = skip loads, 8 = skip reduction/stores, 32 = clock stamps
+#endif
 constexpr int kCfWaves = 8;
 constexpr int kCfThreads = kCfWaves * kWave;
-constexpr int kCfRB = 2;                       // row blocks per tile
-constexpr int kCfTileOut = 128 * kCfRB;        // 256 outputs: 16 output rows x 16 columns
-constexpr int kCfMaxKS = 6;                    // K-steps of 32 per wave: K <= 8 x 6 x 32 = 1536
-constexpr int kCfPartBytes = kCfWaves * 4 * kCfRB * kWave * 4;  // one partial buffer (16 KB)
-constexpr int kCfDynLdsMax = 160 * 1024 - 256;                  // the rest: static flags
+constexpr int kCfTileOut = 512;  // 16 rows x 32 columns
+constexpr int kCfMaxKS = 11;     // K-steps of 16 per wave: K <= 8 x 11 x 16 = 1408
+constexpr int kCfMaxD = 16;
+constexpr int kCfPartialBytes = kCfWaves * 16 * kWave * 4;  // 32 KB
+constexpr int kCfDynLdsMax = 160 * 1024 - 256;             // the rest: static flags
 
 struct CfFirArgs {
-  const float* x;       // interleaved re, im (16-byte aligned)
+  const float* x;     // interleaved re, im
   const float* taps;
   void* out;
   int64_t nOut;
-  int64_t nIn;          // complex samples readable: (nOut - 1) D + T
+  int64_t nIn;        // complex samples readable: (nOut - 1) D + T
   int32_t T;
   int32_t D;
-  int32_t KS;           // K-steps per wave
+  int32_t KS;         // K-steps per wave
   int32_t tiles;
-  int32_t Wu;           // window units (8 samples) per tile = 30 D + 32 KS
-  int32_t padShift;     // plane unit u at u + (u >> padShift) (31: no padding)
-  int32_t planeStride;  // bytes between planes (limb l, component c at 2 l + c)
+  int32_t Wu;         // window units (8 samples) per tile = 60 D + 16 KS
+  int32_t padShift;   // plane unit u lives at u + (u >> padShift)
+  int32_t planeStride;  // bytes between the six planes (limb l, component c at 2 l + c)
 };
+
+__device__ __forceinline__ int cfPhys(int u, int p) { return u + (u >> p); }
 
 // fp32 pair -> three bf16 limb pairs (exact).
 __device__ __forceinline__ void split3(float a, float b, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
@@ -80,18 +77,19 @@ __device__ __forceinline__ void split3(float a, float b, uint32_t& l0, uint32_t&
   l2 = __builtin_bit_cast(uint32_t, h2);
 }
 
-// Window registers: G groups of 8 samples (64 B) per thread, group g = tid + 512 j.
+// Window loads: G groups of 8 samples (64 B) per thread, group g = tid + 512 j.
 template <int G>
 struct CfWindow {
   f4 v[G][4];  // native vector type: HIP's float4 union defeats register promotion
 };
 
-// Branch-free, so the loads stay in flight until the split that consumes them; f4 index
-// arithmetic on the kernel-argument pointer keeps them global_load (a flat load would also count
-// on lgkmcnt and stall the LDS waits of the MFMA loop). Blocks past the input end re-read the last
-// one (their samples feed only outputs >= nOut or meet zero taps); surplus groups repeat the last.
+// Branch-free, so the loads stay in flight until the split that consumes them: blocks past the
+// input end re-read the last 16-byte block holding input bytes (never crossing a page); those
+// samples feed only outputs >= nOut or meet zero taps. Surplus groups (g >= Wu) repeat the last.
 template <int G>
 __device__ __forceinline__ void loadWindow(const CfFirArgs& a, int tile, int tid, CfWindow<G>& w) {
+  // f4 = 2 samples; index arithmetic on the kernel-argument pointer keeps these global_load
+  // (a flat load would also count on lgkmcnt and stall every LDS wait of the MFMA loop)
   const f4* x4 = reinterpret_cast<const f4*>(a.x);
   const int64_t base = (int64_t)tile * kCfTileOut * a.D / 2;
   const int64_t last = (a.nIn - 1) >> 1;
@@ -106,66 +104,41 @@ __device__ __forceinline__ void loadWindow(const CfFirArgs& a, int tile, int tid
   }
 }
 
-__device__ __forceinline__ int cfUnit(int u, int p) { return u + (u >> p); }
-
+// Split the window into the planes; a non-finite sample sets *nonFinite (0 * x is NaN exactly
+// for x = +-inf or NaN), so the tile takes the direct path: the Toeplitz product would multiply
+// the sample by the zero taps of outputs whose windows do not contain it (0 * inf = NaN).
 template <int G>
-__device__ __forceinline__ void splitWindow(const CfFirArgs& a, const CfWindow<G>& w, int8_t* buf, int tid) {
+__device__ __forceinline__ void splitWindow(const CfFirArgs& a, const CfWindow<G>& w, int8_t* planes, int tid,
+                                            int* nonFinite) {
+  f4 probe = f4{};
 #pragma unroll
   for (int j = 0; j < G; ++j) {
-    const int g = min(tid + kCfThreads * j, a.Wu - 1);
-    uint32_t iL[3][4], qL[3][4];
+    const int g = tid + kCfThreads * j;
+    if (g < a.Wu) {
+      uint32_t iL[3][4], qL[3][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {  // samples 2q, 2q + 1: (re, im, re, im)
-      split3(w.v[j][q].x, w.v[j][q].z, iL[0][q], iL[1][q], iL[2][q]);
-      split3(w.v[j][q].y, w.v[j][q].w, qL[0][q], qL[1][q], qL[2][q]);
-    }
-    const int off = 16 * cfUnit(g, a.padShift);
+      for (int q = 0; q < 4; ++q) {  // samples 2q, 2q + 1: (re, im, re, im)
+        split3(w.v[j][q].x, w.v[j][q].z, iL[0][q], iL[1][q], iL[2][q]);
+        split3(w.v[j][q].y, w.v[j][q].w, qL[0][q], qL[1][q], qL[2][q]);
+        probe += w.v[j][q] * 0.0f;
+      }
+      const int off = 16 * cfPhys(g, a.padShift);
 #pragma unroll
-    for (int l = 0; l < 3; ++l) {
-      *reinterpret_cast<uint4*>(buf + (2 * l) * a.planeStride + off) = uint4{iL[l][0], iL[l][1], iL[l][2], iL[l][3]};
-      *reinterpret_cast<uint4*>(buf + (2 * l + 1) * a.planeStride + off) = uint4{qL[l][0], qL[l][1], qL[l][2], qL[l][3]};
-    }
-  }
-}
-
-// This wave's share of one tile: both row blocks over its KS K-steps, 6 MFMAs per K-step and
-// row block, into the partial-sum buffer `part` ([wave][register][lane]).
-__device__ __forceinline__ void tileMfma(const CfFirArgs& a, const int8_t* buf, const bf8 (&bf)[kCfMaxKS][3],
-                                         float* part, int wave, int lane) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  const int r = lane & 15;
-  const int8_t* plane = buf + (r >> 3) * a.planeStride;  // re rows 0-7, im rows 8-15
-  const int uRow = 2 * a.D * (r & 7) + (lane >> 4) + 4 * wave * a.KS;
-  v4f acc[kCfRB];
-#pragma unroll
-  for (int rb = 0; rb < kCfRB; ++rb) acc[rb] = v4f{};
-#pragma unroll
-  for (int s = 0; s < kCfMaxKS; ++s) {
-    if (s < a.KS && !(GSDR_CF_EXPERIMENT & 2)) {
-#pragma unroll
-      for (int rb = 0; rb < kCfRB; ++rb) {
-        const int off = 16 * cfUnit(uRow + 16 * a.D * rb + 4 * s, a.padShift);
-        const bf8 x0 = *reinterpret_cast<const bf8*>(plane + off);
-        const bf8 x1 = *reinterpret_cast<const bf8*>(plane + 2 * a.planeStride + off);
-        const bf8 x2 = *reinterpret_cast<const bf8*>(plane + 4 * a.planeStride + off);
-        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, bf[s][0], acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, bf[s][1], acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, bf[s][0], acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, bf[s][2], acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, bf[s][1], acc[rb], 0, 0, 0);
-        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, bf[s][0], acc[rb], 0, 0, 0);
+      for (int l = 0; l < 3; ++l) {
+        *reinterpret_cast<uint4*>(planes + (2 * l) * a.planeStride + off) = uint4{iL[l][0], iL[l][1], iL[l][2], iL[l][3]};
+        *reinterpret_cast<uint4*>(planes + (2 * l + 1) * a.planeStride + off) =
+            uint4{qL[l][0], qL[l][1], qL[l][2], qL[l][3]};
       }
     }
   }
-#pragma unroll
-  for (int rb = 0; rb < kCfRB; ++rb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) part[(wave * 4 * kCfRB + 4 * rb + i) * kWave + lane] = acc[rb][i];
+  const float pr = (probe.x + probe.y) + (probe.z + probe.w);
+  if (pr != pr) *nonFinite = 1;
 }
 
-// Direct fp32 form of output k (tiles holding a non-finite value).
+// Direct fp32 form of one tile, one output per thread (tiles holding a non-finite sample).
 template <int EPI>
-__device__ __forceinline__ void cfDirectOutput(const CfFirArgs& a, int64_t k) {
+__device__ __forceinline__ void directTile(const CfFirArgs& a, int tile, int tid) {
+  const int64_t k = (int64_t)tile * kCfTileOut + tid;
   if (k >= a.nOut) return;
   const f2* x = reinterpret_cast<const f2*>(a.x) + k * a.D;
   f2 y = f2{0.0f, 0.0f};
@@ -174,17 +147,17 @@ __device__ __forceinline__ void cfDirectOutput(const CfFirArgs& a, int64_t k) {
   else reinterpret_cast<f2*>(a.out)[k] = y;
 }
 
-template <int G, int EPI>
+template <int KS, int G, int EPI>
 __global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  const int bufBytes = 6 * a.planeStride;
-  float* parts = reinterpret_cast<float*>(smem + 2 * bufBytes);  // two partial buffers
-  __shared__ int nonFinite[3];  // per tile mod 3: a reduced output was inf / NaN
+  int8_t* planes = smem;
+  float* part = reinterpret_cast<float*>(smem + 6 * a.planeStride);
+  __shared__ int nonFinite[2];  // per tile parity: the window holds an inf / NaN
 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wave = waveUniform(tid >> 6);
-  const int D = a.D, T = a.T, KS = a.KS;
+  const int D = a.D, T = a.T;
 
   // contiguous tile range of this block
   const int q = a.tiles / (int)gridDim.x, r = a.tiles % (int)gridDim.x;
@@ -192,29 +165,31 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
   const int n = q + ((int)blockIdx.x < r ? 1 : 0);
   if (n <= 0) return;
 
+  // first window in flight while the taps are prepared
   CfWindow<G> win;
   loadWindow<G>(a, t0, tid, win);
 
-  // ---- taps -> LDS (zero-padded to [-15 D, 256 KS)), then this wave's B fragments -------------
-  if (tid < 3) nonFinite[tid] = 0;
-  const int off0 = 15 * D;
-  const int span = off0 + 256 * KS;
+  // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), then this wave's B fragments -------------
+  if (tid < 2) nonFinite[tid] = 0;
+  const int off0 = 31 * D;
+  const int span = off0 + 128 * KS;
   for (int i = tid; i < span; i += kCfThreads) {
     const int j = i - off0;
-    parts[i] = (j >= 0 && j < T) ? a.taps[j] : 0.0f;
+    part[i] = (j >= 0 && j < T) ? a.taps[j] : 0.0f;
   }
   __syncthreads();
-  const int col = lane & 15;
+  const int half = lane >> 5;
+  const int col = lane & 31;
   bf8 bf[kCfMaxKS][3];
 #pragma unroll
   for (int s = 0; s < kCfMaxKS; ++s) {
     if (s < KS) {
-      const int kap = 32 * (wave * KS + s) + 8 * (lane >> 4);  // first kappa of this lane's 8
+      const int kap = 16 * (wave * KS + s) + 8 * half;  // first kappa of this lane's 8
       uint32_t l[3][4];
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        const float h0 = parts[off0 + kap + 2 * p - col * D];
-        const float h1 = parts[off0 + kap + 2 * p + 1 - col * D];
+        const float h0 = part[off0 + kap + 2 * p - col * D];
+        const float h1 = part[off0 + kap + 2 * p + 1 - col * D];
         split3(h0, h1, l[0][p], l[1][p], l[2][p]);
       }
 #pragma unroll
@@ -224,54 +199,76 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
       for (int i = 0; i < 3; ++i) bf[s][i] = bf8{};
     }
   }
-  __syncthreads();  // the tap staging area becomes the partial buffers
+  __syncthreads();  // the tap staging area becomes the partial-sum area
 
-  // ---- prologue: tile t0 into buffer 0, tile t0 + 1's loads in flight ------------------------
-  if (!(GSDR_CF_EXPERIMENT & 1)) splitWindow<G>(a, win, smem, tid);
-  if (n > 1 && !(GSDR_CF_EXPERIMENT & 4)) loadWindow<G>(a, t0 + 1, tid, win);
+  // ---- prologue: tile t0's window into the planes, tile t0 + 1's loads in flight -------------
+  splitWindow<G>(a, win, planes, tid, &nonFinite[t0 & 1]);
+  if (n > 1) loadWindow<G>(a, t0 + 1, tid, win);
   __syncthreads();
+
+  // A-fragment geometry: row r = lane & 15 of component c = (lane >> 4) & 1, K-half `half`
+  const int arow = lane & 15;
+  const int comp = (lane >> 4) & 1;
+  const int uRow = 4 * D * arow + half;
+  const int8_t* pI = planes + comp * a.planeStride;
 
   for (int i = 0; i < n; ++i) {
     const int tile = t0 + i;
-    const int8_t* cur = smem + (i & 1) * bufBytes;
-    int8_t* nxt = smem + ((i + 1) & 1) * bufBytes;
-    float* part = parts + (i & 1) * (kCfPartBytes / 4);
-    const bool splitNext = i + 1 < n && !(GSDR_CF_EXPERIMENT & 1);
-    // waves 0-3 split tile + 1 first, waves 4-7 run their MFMAs first (wave-uniform)
-    if (wave < 4) {
-      if (splitNext) splitWindow<G>(a, win, nxt, tid);
-      tileMfma(a, cur, bf, part, wave, lane);
+    const bool direct = nonFinite[tile & 1] != 0;  // block-uniform (set before the last barrier)
+    if (tid == 0) nonFinite[(tile + 1) & 1] = 0;    // last read in tile - 1's compute
+    if (direct) {
+      directTile<EPI>(a, tile, tid);
+      __syncthreads();  // the flag reset above precedes the next split's writes
     } else {
-      tileMfma(a, cur, bf, part, wave, lane);
-      if (splitNext) splitWindow<G>(a, win, nxt, tid);
-    }
-    if (i + 2 < n && !(GSDR_CF_EXPERIMENT & 4)) loadWindow<G>(a, tile + 2, tid, win);
-    __syncthreads();  // partials of tile, planes of tile + 1 complete
-    if (tid == 0) nonFinite[(i + 1) % 3] = 0;  // tile i - 2's flag, read before this barrier
-
-    if (tid < kCfTileOut) {
-      // tile - 1 left a non-finite output: redo it in the direct form (same thread, same output)
-      if (i > 0 && nonFinite[(i + 2) % 3]) cfDirectOutput<EPI>(a, (int64_t)(tile - 1) * kCfTileOut + tid);
-      // reduction + epilogue: output o = tid of this tile
-      const int o = tid, rb = o >> 7, orow = (o >> 4) & 7;
-      const int laneI = 16 * (orow >> 2) + (o & 15);
-      const int reg = 4 * rb + (orow & 3);
-      float yi = 0.0f, yq = 0.0f;
+    // ---- this wave's K range: KS K-steps x 6 split-precision MFMAs ---------------------------
+    v16f acc = v16f{};
 #pragma unroll
-      for (int v = 0; v < kCfWaves; ++v) {
-        yi += part[(v * 4 * kCfRB + reg) * kWave + laneI];
-        yq += part[(v * 4 * kCfRB + reg) * kWave + laneI + 32];
+    for (int s = 0; s < kCfMaxKS; ++s) {
+      if (s < KS && !(GSDR_CF_EXPERIMENT & 2)) {
+        const int u = uRow + 2 * (wave * KS + s);
+        const int off = 16 * cfPhys(u, a.padShift);
+        const bf8 x0 = *reinterpret_cast<const bf8*>(pI + off);
+        const bf8 x1 = *reinterpret_cast<const bf8*>(pI + 2 * a.planeStride + off);
+        const bf8 x2 = *reinterpret_cast<const bf8*>(pI + 4 * a.planeStride + off);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x0, bf[s][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x0, bf[s][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, bf[s][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x0, bf[s][2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, bf[s][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, bf[s][0], acc, 0, 0, 0);
       }
-      const int64_t k = (int64_t)tile * kCfTileOut + o;
-      if (k < a.nOut) {
-        if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq});
-        else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq};
-        if (!(__builtin_isfinite(yi) && __builtin_isfinite(yq))) nonFinite[i % 3] = 1;
-      }
+    }
+    if (GSDR_CF_EXPERIMENT & 8) {
+      if (acc[0] + acc[7] + acc[13] == 1.2345f) reinterpret_cast<float*>(a.out)[lane] = 0.0f;
+      __syncthreads();
+    } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
+    __syncthreads();  // partials complete; every wave is done reading the planes
+
+    // ---- reduction + epilogue: wave w finishes accumulator register w (I) / w + 8 (Q) --------
+    float yi = 0.0f, yq = 0.0f;
+#pragma unroll
+    for (int v = 0; v < kCfWaves; ++v) {
+      yi += part[(v * 16 + wave) * kWave + lane];
+      yq += part[(v * 16 + wave + 8) * kWave + lane];
+    }
+    const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * half;
+    const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
+    if (k < a.nOut) {
+      if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq});
+      else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq};
+    }
+    }
+    }
+
+    // ---- next tile's window into the planes, the one after into registers ------------------
+    if (i + 1 < n) {
+      if (!(GSDR_CF_EXPERIMENT & 1)) splitWindow<G>(a, win, planes, tid, &nonFinite[(tile + 1) & 1]);
+      if (i + 2 < n && !(GSDR_CF_EXPERIMENT & 4)) loadWindow<G>(a, tile + 2, tid, win);
+      __syncthreads();
     }
   }
-  __syncthreads();
-  if (tid < kCfTileOut && nonFinite[(n - 1) % 3]) cfDirectOutput<EPI>(a, (int64_t)(t0 + n - 1) * kCfTileOut + tid);
 }
 
 // ---- host side ------------------------------------------------------------------------------
@@ -290,41 +287,37 @@ struct CfLayout {
   int planeStride;
 };
 
-// Pick the plane padding and the re/im plane offset that minimise the A-fragment bank conflicts
-// for this (D, KS) within the LDS budget (2 plane buffers + 2 partial buffers).
-CfLayout cfLayout(int D, int KS, int Wu) {
-  CfLayout best{31, 0};
+// Pick the plane padding and the I/Q plane offset that minimise the A-fragment bank conflicts
+// for this (D, KS), within the LDS budget.
+CfLayout cfPlaneLayout(int D, int KS, int Wu) {
+  CfLayout best{4, 0};
   double bestCost = 1e30;
-  const int shifts[] = {31, 6, 5, 4, 3, 2, 1};
-  for (int p : shifts) {
-    const int units = Wu + (p < 31 ? (Wu >> p) : 0) + 1;
+  for (int p = 4; p >= 1; --p) {
+    const int units = Wu + (Wu >> p) + 1;
     const int base = (16 * units + 255) / 256 * 256;
     for (int qoff = 0; qoff < 16; ++qoff) {
       const int stride = base + 16 * qoff;
-      if (2 * 6 * stride + 2 * kCfPartBytes > kCfDynLdsMax) continue;
+      if (6 * stride + kCfPartialBytes > kCfDynLdsMax) continue;
       double cost = 0;
-      for (int rb = 0; rb < kCfRB; ++rb) {
-        for (int s = 0; s < kCfWaves * KS; ++s) {
-          for (const auto& grp : kB128Groups) {
-            int units16[16][4];
-            int cnt[16] = {};
-            int worst = 1;
-            for (int li = 0; li < 16; ++li) {
-              const int l = grp[li];
-              const int rr = l & 15;
-              const int u = 2 * D * ((rr & 7) + 8 * rb) + (l >> 4) + 4 * s;
-              const int unit = u + (p < 31 ? (u >> p) : 0) + ((rr >> 3) ? stride / 16 : 0);
-              const int slot = unit & 15;
-              bool dup = false;
-              for (int c = 0; c < cnt[slot]; ++c) dup |= units16[slot][c] == unit;
-              if (!dup && cnt[slot] < 4) units16[slot][cnt[slot]++] = unit;
-              worst = cnt[slot] > worst ? cnt[slot] : worst;
-            }
-            cost += worst;
+      for (int s = 0; s < kCfWaves * KS; ++s) {
+        for (const auto& grp : kB128Groups) {
+          int slots[16][4];
+          int cnt[16] = {};
+          int worst = 1;
+          for (int li = 0; li < 16; ++li) {
+            const int l = grp[li];
+            const int u = 4 * D * (l & 15) + 2 * s + (l >> 5);
+            const int unit = u + (u >> p) + (((l >> 4) & 1) ? stride / 16 : 0);
+            const int slot = unit & 15;
+            bool dup = false;
+            for (int c = 0; c < cnt[slot]; ++c) dup |= slots[slot][c] == unit;
+            if (!dup && cnt[slot] < 4) slots[slot][cnt[slot]++] = unit;
+            worst = cnt[slot] > worst ? cnt[slot] : worst;
           }
+          cost += worst;
         }
       }
-      cost += 1e-3 * (12.0 * stride) / 1024.0;  // tie-break: less LDS
+      cost += 1e-3 * (6.0 * stride) / 1024.0;  // tie-break: less LDS
       if (cost < bestCost) {
         bestCost = cost;
         best = CfLayout{p, stride};
@@ -334,32 +327,35 @@ CfLayout cfLayout(int D, int KS, int Wu) {
   return best;
 }
 
-template <int G, int EPI>
-hipError_t launchCf(const CfFirArgs& a, size_t lds, int grid, hipStream_t stream) {
+template <int KS, int G, int EPI>
+hipError_t launchCfG(const CfFirArgs& a, size_t lds, int grid, hipStream_t stream) {
   static std::once_flag once;
   static hipError_t attrErr = hipSuccess;
   std::call_once(once, [] {
-    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(&firCfMfmaKernel<G, EPI>),
+    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(&firCfMfmaKernel<KS, G, EPI>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kCfDynLdsMax);
   });
   if (attrErr != hipSuccess) return attrErr;
-  hipLaunchKernelGGL((firCfMfmaKernel<G, EPI>), dim3(grid), dim3(kCfThreads), lds, stream, a);
+  hipLaunchKernelGGL((firCfMfmaKernel<KS, G, EPI>), dim3(grid), dim3(kCfThreads), lds, stream, a);
   return hipGetLastError();
+}
+
+template <int KS>
+hipError_t launchCfKS(const CfFirArgs& a, size_t lds, int grid, int epi, hipStream_t stream) {
+  const int G = (a.Wu + kCfThreads - 1) / kCfThreads;
+  switch (G) {
+    case 1: return epi == kEpiAm ? launchCfG<KS, 1, kEpiAm>(a, lds, grid, stream) : launchCfG<KS, 1, kEpiComplex>(a, lds, grid, stream);
+    case 2: return epi == kEpiAm ? launchCfG<KS, 2, kEpiAm>(a, lds, grid, stream) : launchCfG<KS, 2, kEpiComplex>(a, lds, grid, stream);
+    default: return epi == kEpiAm ? launchCfG<KS, 3, kEpiAm>(a, lds, grid, stream) : launchCfG<KS, 3, kEpiComplex>(a, lds, grid, stream);
+  }
 }
 
 }  // namespace
 
 bool firCfMfmaEligible(size_t tapCount, size_t decimation, const void* in) {
   const size_t d = decimation < 1 ? 1 : decimation;
-  if (tapCount < 64 || d > 32 || 15 * d + tapCount > (size_t)(kCfWaves * kCfMaxKS * 32) ||
-      (reinterpret_cast<uintptr_t>(in) & 15u) != 0)
-    return false;
-  const size_t ksteps = (15 * d + tapCount + 31) / 32;
-  const size_t ks = (ksteps + kCfWaves - 1) / kCfWaves;
-  const size_t wu = 30 * d + 32 * ks;
-  if (wu > 2 * (size_t)kCfThreads) return false;  // window registers: at most 2 groups per thread
-  const size_t stride = (16 * (wu + 1) + 255) / 256 * 256 + 16 * 15;  // unpadded, worst offset
-  return 12 * stride + 2 * kCfPartBytes <= (size_t)kCfDynLdsMax;
+  return tapCount >= 64 && d <= (size_t)kCfMaxD && 31 * d + tapCount <= (size_t)(kCfWaves * kCfMaxKS * 16) &&
+         (reinterpret_cast<uintptr_t>(in) & 15u) == 0;
 }
 
 hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, size_t decimation, void* out,
@@ -372,31 +368,41 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
   a.T = (int32_t)tapCount;
   a.nOut = (int64_t)nOut;
   a.nIn = (int64_t)(nOut - 1) * a.D + (int64_t)tapCount;
-  const int ksteps = (15 * a.D + a.T + 31) / 32;
+  const int ksteps = (31 * a.D + a.T + 15) / 16;
   a.KS = (ksteps + kCfWaves - 1) / kCfWaves;
   const int64_t tiles = ((int64_t)nOut + kCfTileOut - 1) / kCfTileOut;
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
   a.tiles = (int32_t)tiles;
-  a.Wu = 30 * a.D + 32 * a.KS;
+  a.Wu = 60 * a.D + 16 * a.KS;
   static std::mutex mu;
   static int cachedD = -1, cachedKS = -1;
   static CfLayout cached{};
   {
     std::lock_guard<std::mutex> lock(mu);
     if (cachedD != a.D || cachedKS != a.KS) {
-      cached = cfLayout(a.D, a.KS, a.Wu);
+      cached = cfPlaneLayout(a.D, a.KS, a.Wu);
       cachedD = a.D;
       cachedKS = a.KS;
     }
     a.padShift = cached.padShift;
     a.planeStride = cached.planeStride;
   }
-  if (a.planeStride == 0) return hipErrorInvalidValue;
-  const size_t lds = 12 * (size_t)a.planeStride + 2 * kCfPartBytes;
+  const size_t lds = 6 * (size_t)a.planeStride + kCfPartialBytes;
+  if (a.planeStride == 0 || lds > (size_t)kCfDynLdsMax) return hipErrorInvalidValue;
   const int grid = (int)(tiles < 256 ? tiles : 256);
-  if (a.Wu <= kCfThreads)
-    return epi == kEpiAm ? launchCf<1, kEpiAm>(a, lds, grid, stream) : launchCf<1, kEpiComplex>(a, lds, grid, stream);
-  return epi == kEpiAm ? launchCf<2, kEpiAm>(a, lds, grid, stream) : launchCf<2, kEpiComplex>(a, lds, grid, stream);
+  switch (a.KS) {
+    case 1: return launchCfKS<1>(a, lds, grid, epi, stream);
+    case 2: return launchCfKS<2>(a, lds, grid, epi, stream);
+    case 3: return launchCfKS<3>(a, lds, grid, epi, stream);
+    case 4: return launchCfKS<4>(a, lds, grid, epi, stream);
+    case 5: return launchCfKS<5>(a, lds, grid, epi, stream);
+    case 6: return launchCfKS<6>(a, lds, grid, epi, stream);
+    case 7: return launchCfKS<7>(a, lds, grid, epi, stream);
+    case 8: return launchCfKS<8>(a, lds, grid, epi, stream);
+    case 9: return launchCfKS<9>(a, lds, grid, epi, stream);
+    case 10: return launchCfKS<10>(a, lds, grid, epi, stream);
+    default: return launchCfKS<11>(a, lds, grid, epi, stream);
+  }
 }
 
 }  // namespace gsdr_amd

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
+#include <cstring>
 
 #define DECL(N)                                                                                    \
   namespace c##N {                                                                                 \
@@ -41,6 +42,14 @@ int main() {
       float ms = 0;
       hipEventElapsedTime(&ms, e0, e1);
       printf("%s %-32s %9.1f us/launch  %s\n", sh.name, v.name, 1000.0f * ms / reps, hipGetErrorString(hipGetLastError()));
+      if (strstr(v.name, "stamp")) {  // block 0: per wave [work, barrier, reduce] cycles, tiles
+        uint32_t st[32];
+        hipMemcpy(st, out, sizeof(st), hipMemcpyDeviceToHost);
+        for (int w = 0; w < 8; ++w)
+          printf("   wave %d: vec %u mfma %u barrier %u cycles over %u tiles (%.0f / %.0f / %.0f per tile)\n", w,
+                 st[4 * w], st[4 * w + 1], st[4 * w + 2], st[4 * w + 3], (double)st[4 * w] / st[4 * w + 3],
+                 (double)st[4 * w + 1] / st[4 * w + 3], (double)st[4 * w + 2] / st[4 * w + 3]);
+      }
     }
     hipFree(x);
     hipFree(taps);
