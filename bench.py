@@ -154,11 +154,18 @@ class ShardedChain:
         if self.mfma_int8:
             s = (self.T + 62) // 32  # K-blocks of 32: K = 32 S >= T + 31
             return in_bytes + n * 4, n * 2 * 2 * 32 * s * 2  # I and Q rows x 2 f16 limbs x K MACs x 2
+        if self.mfma_cf:
+            ks = -(-(-(-(31 * self.D + self.T) // 16)) // 8)  # K-steps of 16 per wave, 8 waves
+            return in_bytes + n * 4, n * 2 * (8 * ks * 16) * 6 * 2  # I/Q rows x K x 6 bf16 products x 2
         return in_bytes + n * 4, n * self.T * 4
 
     @property
     def mfma_int8(self):
         return self.kind == "i8" and self.D == 1 and self.T <= 129
+
+    @property
+    def mfma_cf(self):
+        return self.kind == "c64" and self.T >= 64 and self.D <= 16 and 31 * self.D + self.T <= 1408
 
 
 def cpu_baseline(wl, seconds_target=8.0):
@@ -202,7 +209,7 @@ def cpu_baseline(wl, seconds_target=8.0):
 def kernel_name(chain):
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"
-    body = "firI8MfmaKernel" if chain.mfma_int8 else "firLdsKernel"
+    body = "firI8MfmaKernel" if chain.mfma_int8 else ("firCfMfmaKernel" if chain.mfma_cf else "firLdsKernel")
     return f"{entry} ({body})"
 
 
@@ -299,6 +306,9 @@ def main():
                 "compute": ({"kind": "f16 MFMA (2 tap limbs, fp32 accumulate)", "achieved_tflops": achieved_t,
                              "peak_tflops": F16_PEAK_TFLOPS, "frac": achieved_t / F16_PEAK_TFLOPS,
                              "flops_per_launch": ops_} if chain.mfma_int8 else
+                            {"kind": "bf16 MFMA (3x3 limb split, 6 products, fp32 accumulate)",
+                             "achieved_tflops": achieved_t, "peak_tflops": F16_PEAK_TFLOPS,
+                             "frac": achieved_t / F16_PEAK_TFLOPS, "flops_per_launch": ops_} if chain.mfma_cf else
                             {"kind": "fp32 VALU FMA", "achieved_tflops": achieved_t,
                              "peak_tflops": FP32_PEAK_TFLOPS, "frac": achieved_t / FP32_PEAK_TFLOPS,
                              "flops_per_launch": ops_}),

@@ -224,6 +224,58 @@ def test_int8_mfma_misaligned_falls_back(ops, orc):
         _check_fir(y, y64, bound, ("misaligned", off))
 
 
+CF_MFMA_CASES = [(64, 1, 1000), (127, 3, 5000), (255, 2, 777), (1023, 10, 20000), (1023, 1, 4113),
+                 (600, 16, 3000), (1023, 5, 1), (300, 7, 2049)]
+
+
+@pytest.mark.parametrize("T,D,n_out", CF_MFMA_CASES)
+def test_cf_mfma_path(ops, orc, T, D, n_out):
+    """Split-precision bf16 MFMA FIR (cf32 x real taps, T >= 64): against the float64 oracle,
+    the AM epilogue bit-identical to AM of the complex output, and against the fp32 VALU kernel."""
+    rng = np.random.default_rng(T * 11 + D)
+    n_in = (n_out - 1) * D + T
+    x = (rng.standard_normal(n_in) + 1j * rng.standard_normal(n_in)).astype(np.complex64)
+    taps = orc.lowpass_taps(T, 0.4 / D).astype(np.float32)
+    x_d, taps_d = _dev(x), _dev(taps)
+    y = _host(ops.fir(taps_d, x_d, D, n_out))
+    am = _host(ops.fir(taps_d, x_d, D, n_out, am=True))
+    y64, bound = orc.fir_f64(taps, x, D, n_out)
+    _check_fir(y, y64, bound, ("cf-mfma", T, D, n_out))
+    assert am.tobytes() == orc.quad_am_demod(y).tobytes()
+    prev = ops.set_kernel_policy(ops.POLICY_NO_MFMA)
+    try:
+        y_valu = _host(ops.fir(taps_d, x_d, D, n_out))
+    finally:
+        ops.set_kernel_policy(prev)
+    assert np.all(np.abs(y.astype(np.complex128) - y_valu) <= 2 * FIR_TOL * bound + 1e-30)
+
+
+def test_cf_mfma_dynamic_range(ops, orc):
+    """Bursts 1e6 apart in amplitude inside one tile window: the bf16 x 3 split keeps every
+    output within 1e-6 of its OWN window's sum |h||x| (a scaled f16 split would not)."""
+    T, D, n_out = 1023, 10, 12000
+    rng = np.random.default_rng(5)
+    n_in = (n_out - 1) * D + T
+    x = (rng.standard_normal(n_in) + 1j * rng.standard_normal(n_in)).astype(np.complex64)
+    amp = np.where((np.arange(n_in) // 3000) % 2 == 0, 1.0, 1e-6).astype(np.float32)
+    x = (x * amp).astype(np.complex64)
+    taps = orc.lowpass_taps(T, 0.04).astype(np.float32)
+    y = _host(ops.fir(_dev(taps), _dev(x), D, n_out))
+    y64, bound = orc.fir_f64(taps, x, D, n_out)
+    _check_fir(y, y64, bound, "dynamic-range")
+
+
+def test_cf_mfma_misaligned_falls_back(ops, orc):
+    T, D, n_out = 255, 4, 3000
+    rng = np.random.default_rng(9)
+    n_in = (n_out - 1) * D + T
+    x = (rng.standard_normal(n_in + 1) + 1j * rng.standard_normal(n_in + 1)).astype(np.complex64)
+    taps = orc.lowpass_taps(T, 0.1).astype(np.float32)
+    y = _host(ops.fir(_dev(taps), _dev(x)[1:], D, n_out))  # 8-byte aligned: the VALU kernel
+    y64, bound = orc.fir_f64(taps, x[1:], D, n_out)
+    _check_fir(y, y64, bound, "cf-misaligned")
+
+
 @pytest.mark.parametrize("T,L,mfma", [(127, 10000, True), (127, 50, True), (33, 4099, True), (127, 10000, False),
                                        (1, 300, True)])
 def test_fir_carry_streaming(ops, orc, T, L, mfma):
