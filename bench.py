@@ -8,7 +8,7 @@ The whole chain runs as the fused gfx950 kernel gsdrInt8FirFCAmDemod (== the cha
 gsdrInt8ToNormFloat -> gsdrFirFC -> gsdrQuadAmDemod, bit for bit; tests/test_gpu_parity.py).
 
 One GPU: the step is ONE launch over the buffer [T-1 history | segment] that also writes the
-history for the next step (gsdrInt8FirFCAmDemodCarry; for T <= 129, D = 1 the exact int8 MFMA
+history for the next step (gsdrInt8FirFCAmDemodCarry; for T <= 129, D = 1 the exact f16 MFMA
 kernel firI8MfmaKernel).
 
 Multi-GPU (one process per GPU, torch.distributed over RCCL): the stream is time-sharded.

@@ -27,8 +27,9 @@
 // (~10 us of matrix-core time for 20 M outputs), below the ~20 us the 6-byte-per-sample HBM
 // stream takes; the epilogue is 4 VALU operations per output.
 //
-// Data movement. Each block owns a contiguous range of 4096-output chunks (their windows
-// overlap by T - 1 samples, an L2 hit). The raw interleaved window of a chunk goes HBM -> LDS by
+// Data movement. Each block owns a contiguous range of 512-output tiles (the ranges differ by at
+// most one tile, so no block runs a whole chunk longer than another) and walks it in chunks of
+// up to 4096 outputs (their windows overlap by T - 1 samples, an L2 hit). The raw interleaved window of a chunk goes HBM -> LDS by
 // LDS-DMA (global_load_lds_dwordx4, no VGPRs) into a ring of kRing slots filled kRing - 1 chunks
 // ahead, so the loads of the next chunks stay in flight across the MFMA work and the barriers;
 // one pass per chunk then clamps, converts and splits the slot into the f16 I / Q planes. The
@@ -60,13 +61,12 @@ constexpr int kI8TileOut = 512;                                        // 16 row
 #endif
 #ifndef GSDR_I8_EXPERIMENT
 #define GSDR_I8_EXPERIMENT 0  // attribution builds only: 1 = skip split, 2 = skip MFMA, 4 = skip epilogue,
-                              // 8 = no DMA (compute on stale LDS), 16 = no stores, 32 = clock stamps
-#endif
-#ifndef GSDR_I8_PIPE
-#define GSDR_I8_PIPE 0  // 1: a tile's MFMAs overlap the previous tile's epilogue (sched_group_barrier)
+                              // 8 = no DMA (compute on stale LDS), 16 = no stores, 32 = clock stamps,
+                              // 64 = hi limb only (half the MFMAs), 128 = one A fragment read per tile
 #endif
 constexpr int kI8TilesPerWave = GSDR_I8_TILES_PER_WAVE;
-constexpr int kI8ChunkOut = kI8Waves * kI8TilesPerWave * kI8TileOut;  // 4096 outputs per chunk
+constexpr int kI8ChunkTiles = kI8Waves * kI8TilesPerWave;              // 8 tiles per chunk
+constexpr int kI8ChunkOut = kI8ChunkTiles * kI8TileOut;                // 4096 outputs per chunk
 constexpr int kI8MaxS = 5;                                             // K <= 160 -> T <= 129
 constexpr int kRing = GSDR_I8_RING;                                    // LDS-DMA ring slots
 constexpr int kPiece = 64 * 16;                                        // bytes per wave DMA instruction
@@ -86,7 +86,7 @@ struct I8FirArgs {
   int64_t nOut;
   int64_t nIn;        // complex samples readable: nOut - 1 + T
   int32_t T;
-  int32_t chunks;
+  int32_t tiles;      // ceil(nOut / 512)
   int8_t* carryDst;   // nullptr, or where the last T - 1 input samples go (may alias iq[0 .. T-1))
 };
 
@@ -147,15 +147,16 @@ __device__ __forceinline__ void dmaPiece(const void* src, uint32_t ldsDst) {
       : "memory");
 }
 
-// Issue this wave's DMA pieces of chunk c's raw window into the slot at `slotLds` (LDS byte
-// address, moved down by the dword part of the input's misalignment, so the window starts at
-// the slot's nominal start + (shift & 3)). Lanes past the input end re-read the last 16-byte
-// block that holds input bytes (it never crosses a page); those bytes only feed outputs >= nOut.
+// Issue this wave's DMA pieces of the raw window of the chunk starting at tile `tile` into the
+// slot at `slotLds` (LDS byte address, moved down by the dword part of the input's misalignment,
+// so the window starts at the slot's nominal start + (shift & 3)). Lanes past the last 16-byte
+// block this block's outputs need (`lastBlock`) re-read it (it never crosses a page); those
+// bytes only feed outputs of other blocks or >= nOut, which this block does not store.
 template <int S>
-__device__ __forceinline__ void issueChunk(uintptr_t alignedBase, uintptr_t lastBlock, int c, uint32_t slotLds,
+__device__ __forceinline__ void issueChunk(uintptr_t alignedBase, uintptr_t lastBlock, int tile, uint32_t slotLds,
                                            int wave, int lane) {
   using G = I8Geom<S>;
-  const uintptr_t chunkBase = alignedBase + (uintptr_t)c * (2 * kI8ChunkOut);
+  const uintptr_t chunkBase = alignedBase + (uintptr_t)tile * (2 * kI8TileOut);
 #pragma unroll
   for (int p0 = 0; p0 < G::kPieces; p0 += kI8Waves) {
     const int p = p0 + wave;
@@ -231,13 +232,16 @@ __device__ __forceinline__ void tileMfma(const int8_t* planes, const h8 (&bf)[S]
   const int8_t* plane = planes + (row >> 4) * kPlaneBytes;
   const int b0 = tile * 16 + (row & 15);
   acc = v16f{};
+  h8 a0 = h8{};
+  if (GSDR_I8_EXPERIMENT & 128) a0 = *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0, half));
 #pragma unroll
   for (int s = 0; s < S; ++s) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const h8 av = *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0 + s, 2 * u + half));
+      const h8 av = (GSDR_I8_EXPERIMENT & 128) ? a0 + (_Float16)s
+                                               : *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0 + s, 2 * u + half));
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][1], acc, 0, 0, 0);
+      if (!(GSDR_I8_EXPERIMENT & 64)) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][1], acc, 0, 0, 0);
     }
   }
 }
@@ -260,53 +264,6 @@ __device__ __forceinline__ void tileEpilogue(const I8FirArgs& a, const v16f& acc
         reinterpret_cast<f2*>(a.out)[k] = f2{acc[i], acc[i + 8]} * outScale;
       }
     }
-  }
-}
-
-// One software-pipeline stage of a wave: the MFMAs of `tile` into accNew with the epilogue of
-// the previous tile (accOld, outputs from oldOut) placed between them by hand: sched_barrier(0)
-// fences pin the order, so the vector ALU works while the matrix pipe runs (an MFMA holds the
-// SIMD's vector issue for only 8 of its 32 cycles).
-template <int S, int EPI>
-__device__ __forceinline__ void pipeStage(const I8FirArgs& a, const int8_t* planes, const h8 (&bf)[S][2][2],
-                                          int tile, v16f& accNew, const v16f& accOld, int64_t oldOut, bool haveOld,
-                                          int lane, float outScale) {
-  if (haveOld && oldOut + kI8TileOut <= a.nOut) {  // wave-uniform steady state
-    constexpr int kPlaneBytes = I8Geom<S>::kPlaneBytes;
-    const int row = lane & 31;
-    const int half = lane >> 5;
-    const int8_t* plane = planes + (row >> 4) * kPlaneBytes;
-    const int b0 = tile * 16 + (row & 15);
-    const int64_t rowOut = oldOut + 4 * half * 32 + (lane & 31);
-    auto frag = [&](int j) {  // K-half j = 2 s + u
-      return *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0 + (j >> 1), 2 * (j & 1) + half));
-    };
-    auto out = [&](int i) {  // epilogue of output register i of the old tile
-      const int64_t k = rowOut + 32 * ((i & 3) + 8 * (i >> 2));
-      if (EPI == kEpiAm) {
-        const float m2 = fmaf(accOld[i], accOld[i], accOld[i + 8] * accOld[i + 8]);
-        reinterpret_cast<float*>(a.out)[k] = __builtin_amdgcn_sqrtf(m2) * outScale;
-      } else {
-        reinterpret_cast<f2*>(a.out)[k] = f2{accOld[i], accOld[i + 8]} * outScale;
-      }
-    };
-    h8 f0 = frag(0), f1 = frag(1), f2v;
-    accNew = v16f{};
-#pragma unroll
-    for (int j = 0; j < 2 * S; ++j) {
-      if (j + 2 < 2 * S) f2v = frag(j + 2);
-      accNew = __builtin_amdgcn_mfma_f32_32x32x16_f16(f0, bf[j >> 1][j & 1][0], accNew, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (j < 8) out(j);
-      __builtin_amdgcn_sched_barrier(0);
-      accNew = __builtin_amdgcn_mfma_f32_32x32x16_f16(f0, bf[j >> 1][j & 1][1], accNew, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      f0 = f1;
-      f1 = f2v;
-    }
-  } else {
-    tileMfma<S>(planes, bf, tile, lane, accNew);
-    if (haveOld) tileEpilogue<EPI, false>(a, accOld, oldOut, lane, outScale);
   }
 }
 
@@ -350,13 +307,14 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
   const int wave = waveUniform(tid >> 6);
   const int T = a.T;
 
-  // this block's contiguous chunk range
-  // (q chunks each, one more for the first r blocks: with blocks b, b + 256, b + 512 sharing a CU
+  // this block's contiguous tile range [T0, T0 + nt), walked in n chunks of up to 8 tiles
+  // (q tiles each, one more for the first r blocks: with blocks b, b + 256, b + 512 sharing a CU
   // under round-robin dispatch, the surplus spreads one per CU first - a speed heuristic only)
-  const int q = a.chunks / (int)gridDim.x, r = a.chunks % (int)gridDim.x;
-  const int G0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
-  const int n = q + ((int)blockIdx.x < r ? 1 : 0);
-  if (n <= 0) return;  // block-uniform, before any barrier or DMA
+  const int q = a.tiles / (int)gridDim.x, r = a.tiles % (int)gridDim.x;
+  const int T0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
+  const int nt = q + ((int)blockIdx.x < r ? 1 : 0);
+  if (nt <= 0) return;  // block-uniform, before any barrier or DMA
+  const int n = (nt + kI8ChunkTiles - 1) / kI8ChunkTiles;
 
   // ---- tap load, then the ring prologue (chunks 0 .. kRing-2 of the range) -------------------
   // The tap load is an asm load too, so no compiler-inserted vmcnt(0) drains the DMA: it is
@@ -365,7 +323,10 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
   const uintptr_t base = reinterpret_cast<uintptr_t>(a.iq);
   const int shift = (int)(base & 15u);
   const uintptr_t alignedBase = base - shift;
-  const uintptr_t lastBlock = (base + 2 * (uintptr_t)a.nIn - 1) & ~(uintptr_t)15;
+  // last byte any output of this block reads: sample (T0 + nt) 512 + 32 S - 32 - 1 (K = 32 S
+  // covers the T - 1 history), capped at the input end
+  const int64_t needEnd = min((int64_t)(T0 + nt) * kI8TileOut + 32 * S - 32, a.nIn);
+  const uintptr_t lastBlock = (base + 2 * (uintptr_t)needEnd - 1) & ~(uintptr_t)15;
   // slot j's window starts at ring + kRingPad + j kSlot + (shift & 3): the DMA destination moves
   // down by the dword part of the misalignment (into the previous slot's unused tail / the pad)
   const uint32_t ringLds =
@@ -377,7 +338,7 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
 #pragma unroll
   for (int j = 0; j < kRing - 1; ++j)
     if (j < n && !(GSDR_I8_EXPERIMENT & 8))
-      issueChunk<S>(alignedBase, lastBlock, G0 + j, ringLds + j * G::kSlot, wave, lane);
+      issueChunk<S>(alignedBase, lastBlock, T0 + j * kI8ChunkTiles, ringLds + j * G::kSlot, wave, lane);
   reinterpret_cast<uint32_t*>(limbTab)[tid] = 0u;  // 2 rows x 256 f16 = one dword per thread
   vmWaitDyn<0, (kRing - 1) * kMaxPerChunk>(waveUniform(min(kRing - 1, n) * perChunk));
   asm volatile("" : "+v"(hv));  // hv is defined only after the wait
@@ -433,20 +394,18 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
     t0r = __builtin_amdgcn_s_memrealtime();
   }
   (void)tStart;
-  v16f accPrev = v16f{};
-  int64_t prevOut = 0;
   for (int i = 0; i < n; ++i) {
     // Retire slot i: after its pieces this wave issued min(kRing-2, n-1-i) later chunks' pieces
     // and the stores of min(i, kRing-1) chunks (stores of chunk j follow the pieces of j+kRing-1).
-    const int later = min(kRing - 2, n - 1 - i) * perChunk + min(i, kRing - 1) * kStoresPerChunk -
-                      ((GSDR_I8_PIPE && i > 0 && i <= kRing - 1) ? kStoresPerChunk / 2 : 0);
+    // (only the last chunk may be partial: its stores follow every wait but the final one)
+    const int later = min(kRing - 2, n - 1 - i) * perChunk + min(i, kRing - 1) * kStoresPerChunk;
     if (GSDR_I8_EXPERIMENT & 8) {
     } else if (later == kSteady) vmWait<kSteady>();  // the steady state of the widest waves
     else vmWaitDyn<0, kSteady>(waveUniform(later));
     ldsBarrier();  // every wave's pieces of slot i landed; compute(i-1) done with the planes
     const int slot = i % kRing;
     if (!(GSDR_I8_EXPERIMENT & 1)) splitSlot<S>(ring + kRingPad + slot * G::kSlot + sub, planes, sub, tid);
-    if (a.carryDst != nullptr && G0 == 0 && i == 0) {
+    if (a.carryDst != nullptr && T0 == 0 && i == 0) {
       // streaming history: the only block that reads samples [0, T - 1) has them in LDS now,
       // so the carry may overwrite them in place (source [nOut, nIn) is disjoint: nOut >= T - 1)
       const uint16_t* src = reinterpret_cast<const uint16_t*>(a.iq) + (a.nIn - (T - 1));
@@ -454,26 +413,18 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
     }
     // refill the slot chunk i-1 used (its split finished before the barrier above)
     if (i + kRing - 1 < n && !(GSDR_I8_EXPERIMENT & 8))
-      issueChunk<S>(alignedBase, lastBlock, G0 + i + kRing - 1, ringLds + ((i + kRing - 1) % kRing) * G::kSlot,
-                    wave, lane);
+      issueChunk<S>(alignedBase, lastBlock, T0 + (i + kRing - 1) * kI8ChunkTiles,
+                    ringLds + ((i + kRing - 1) % kRing) * G::kSlot, wave, lane);
     ldsBarrier();  // planes complete
-    const int64_t chunkOut = (int64_t)(G0 + i) * kI8ChunkOut;
-    if constexpr (GSDR_I8_PIPE) {
-      static_assert(!GSDR_I8_PIPE || kI8TilesPerWave == 2, "the pipelined path pairs two tiles per wave");
-      const int t0 = 2 * wave;
-      v16f accA, accB;
-      pipeStage<S, EPI>(a, planes, bf, t0, accA, accPrev, prevOut, i > 0, lane, outScale);
-      pipeStage<S, EPI>(a, planes, bf, t0 + 1, accB, accA, chunkOut + (int64_t)t0 * kI8TileOut, true, lane,
-                        outScale);
-      accPrev = accB;
-      prevOut = chunkOut + (int64_t)(t0 + 1) * kI8TileOut;
-    } else {
+    const int c0 = T0 + i * kI8ChunkTiles;
+    const int ct = min(kI8ChunkTiles, T0 + nt - c0);  // tiles in this chunk (< 8 only for the last)
+    const int64_t chunkOut = (int64_t)c0 * kI8TileOut;
 #pragma unroll
-      for (int t = 0; t < kI8TilesPerWave; ++t)
-        computeTile<S, EPI>(a, planes, bf, chunkOut, wave * kI8TilesPerWave + t, lane, outScale);
+    for (int t = 0; t < kI8TilesPerWave; ++t) {
+      const int tile = wave + kI8Waves * t;  // a partial chunk spreads over the waves
+      if (tile < ct) computeTile<S, EPI>(a, planes, bf, chunkOut, tile, lane, outScale);
     }
   }
-  if constexpr (GSDR_I8_PIPE) tileEpilogue<EPI, false>(a, accPrev, prevOut, lane, outScale);
   vmWait<0>();  // no DMA may still target this block's LDS when it exits
   if ((GSDR_I8_EXPERIMENT & 32) && tid == 0) {
     const uint64_t tc = __builtin_amdgcn_s_memtime(), tr = __builtin_amdgcn_s_memrealtime();
@@ -515,11 +466,11 @@ hipError_t launchFirI8Mfma(const int8_t* iq, const float* taps, size_t tapCount,
   a.nOut = (int64_t)nOut;
   a.nIn = (int64_t)nOut - 1 + (int64_t)tapCount;
   a.T = (int32_t)tapCount;
-  const int64_t chunks = ((int64_t)nOut + kI8ChunkOut - 1) / kI8ChunkOut;
-  if (chunks > 0x7fffffff) return hipErrorInvalidValue;
-  a.chunks = (int32_t)chunks;
-  // 3 resident blocks per CU (<= 168 VGPRs); each streams a contiguous chunk range
-  const int grid = (int)(chunks < 256 * GSDR_I8_BLOCKS_PER_CU ? chunks : 256 * GSDR_I8_BLOCKS_PER_CU);
+  const int64_t tiles = ((int64_t)nOut + kI8TileOut - 1) / kI8TileOut;
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  a.tiles = (int32_t)tiles;
+  // 3 resident blocks per CU (<= 168 VGPRs); each streams a contiguous tile range
+  const int grid = (int)(tiles < 256 * GSDR_I8_BLOCKS_PER_CU ? tiles : 256 * GSDR_I8_BLOCKS_PER_CU);
   const int S = (int)((tapCount + 31 + 31) / 32);
   switch (S) {
     case 1: return launchI8<1>(a, epi, stream, grid);

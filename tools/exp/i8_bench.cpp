@@ -36,9 +36,9 @@ int main() {
   hipEventCreate(&e1);
   const int8_t* src = iq + 252;  // the bench's [126-sample history | segment] offset
   for (auto& v : vars) {
-    for (int w = 0; w < 3; ++w) v.fn(src, taps, T, out, nOut, 2, 0, nullptr);
+    for (int w = 0; w < (getenv("WARM") ? atoi(getenv("WARM")) : 3); ++w) v.fn(src, taps, T, out, nOut, 2, 0, nullptr);
     hipDeviceSynchronize();
-    const int reps = 20;
+    const int reps = getenv("REPS") ? atoi(getenv("REPS")) : 20;
     hipEventRecord(e0, 0);
     for (int r = 0; r < reps; ++r) v.fn(src, taps, T, out, nOut, 2, 0, nullptr);
     hipEventRecord(e1, 0);

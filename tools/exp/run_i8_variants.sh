@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build and time variants of csrc/kernels/fir_i8_mfma.hip: each line of VARIANTS is
-# "name|extra flags"; every variant is compiled into its own namespace (-Dgsdr_amd=vN).
+# "name|extra flags[|source file]"; every variant is compiled into its own namespace (-Dgsdr_amd=vN).
 # Usage: bash tools/exp/run_i8_variants.sh build   (here, cross-compile)
 #        bash tools/exp/run_i8_variants.sh run     (GPU box)
 set -eu
@@ -9,17 +9,16 @@ OUT=tools/exp/_build
 KSRC=cuda-sdr_amd/csrc/kernels/fir_i8_mfma.hip
 VARIANTS=${VARIANTS:-"base|
 base_clk|-DGSDR_I8_EXPERIMENT=32
-pipe|-DGSDR_I8_PIPE=1
 bpc2|-DGSDR_I8_BLOCKS_PER_CU=2
 tiles1|-DGSDR_I8_TILES_PER_WAVE=1
 tiles1_clk|-DGSDR_I8_TILES_PER_WAVE=1 -DGSDR_I8_EXPERIMENT=32"}
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
   decls=""; table=""; objs=""; i=0
-  while IFS='|' read -r name flags; do
+  while IFS='|' read -r name flags src; do
     [ -z "$name" ] && continue
     hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Iinclude -Icuda-sdr_amd/csrc/kernels -mllvm -amdgpu-mfma-vgpr-form \
-      -Dgsdr_amd=v$i $flags -c $KSRC -o $OUT/v$i.o &
+      -Dgsdr_amd=v$i $flags -c ${src:-$KSRC} -o $OUT/v$i.o &
     decls="$decls DECL($i)"; table="$table {\"$name\", v$i::launchFirI8Mfma},"; objs="$objs $OUT/v$i.o"
     i=$((i+1))
   done <<< "$VARIANTS"
