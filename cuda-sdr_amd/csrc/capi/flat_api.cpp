@@ -201,4 +201,40 @@ uint32_t gspBufferToHost(gspHandle buffer, void* host, size_t bytes, gspHandle q
   return Status_Success;
 }
 
+
+uint32_t gspSteppingDriverCreate(gspHandle* driverOut) {
+  return give(factories()->getSteppingDriverFactory()->createSteppingDriver(), driverOut);
+}
+
+uint32_t gspDriverConnect(gspHandle driver, gspHandle source, size_t sourcePort, gspHandle sink, size_t sinkPort) {
+  IDriver* d = as<IDriver>(driver);
+  Source* so = as<Source>(source);
+  Sink* si = as<Sink>(sink);
+  if (d == nullptr || so == nullptr || si == nullptr) return Status_InvalidArgument;
+  return d->connect(so, sourcePort, si, sinkPort);
+}
+
+uint32_t gspDriverSetupNode(gspHandle driver, gspHandle node, const char* name) {
+  IDriver* d = as<IDriver>(driver);
+  Node* n = as<Node>(node);
+  if (d == nullptr || n == nullptr) return Status_InvalidArgument;
+  return d->setupNode(n, name);
+}
+
+uint32_t gspDriverDoFilter(gspHandle driver) {
+  ISteppingDriver* d = as<ISteppingDriver>(driver);
+  if (d == nullptr) return Status_InvalidArgument;
+  return d->doFilter();
+}
+
+size_t gspDriverNodeName(gspHandle driver, gspHandle node, char* name, size_t nameBufLen, int32_t* found) {
+  IDriver* d = as<IDriver>(driver);
+  Node* n = as<Node>(node);
+  bool f = false;
+  size_t len = 0;
+  if (d != nullptr && n != nullptr) len = d->getNodeName(n, name, nameBufLen, &f);
+  if (found != nullptr) *found = f ? 1 : 0;
+  return len;
+}
+
 }  // extern "C"

@@ -1,0 +1,243 @@
+// SteppingDriver (reference src/driver/SteppingDriver.cpp:102-496); see driver.h for the
+// differences from the reference.
+#include "driver.h"
+
+#include <gpusdrpipeline/abi/errors.h>
+
+#include <algorithm>
+#include <cstring>
+
+namespace gsdr_rt {
+
+namespace {
+constexpr int kMaxDepth = 1024;  // longer upstream chains than this are treated as a cycle
+const char kUnnamed[] = "NOT SET";  // SteppingDriver.cpp:30
+}  // namespace
+
+SteppingDriver::SourceInfo& SteppingDriver::sourceInfo(Source* source) {
+  auto [it, inserted] = mSources.try_emplace(source, source);
+  if (inserted) mSourceOrder.push_back(source);
+  return it->second;
+}
+
+SteppingDriver::SinkInfo& SteppingDriver::sinkInfo(Sink* sink) { return mSinks.try_emplace(sink, sink).first->second; }
+
+const char* SteppingDriver::nameOf(Node* node) const noexcept {
+  auto it = mNodes.find(node);
+  return it == mNodes.end() ? kUnnamed : it->second.name.c_str();
+}
+
+// SteppingDriver.cpp:102-135. A sink port takes one upstream; connecting a second is InvalidState.
+Status SteppingDriver::connect(Source* source, size_t sourcePort, Sink* sink, size_t sinkPort) noexcept {
+  if (source == nullptr || sink == nullptr) {
+    gsloge("SteppingDriver::connect: source and sink must not be null");
+    return Status_InvalidArgument;
+  }
+  try {
+    auto existing = mSinks.find(sink);
+    if (existing != mSinks.end() && sinkPort < existing->second.inputs.size() &&
+        existing->second.inputs[sinkPort].source != nullptr) {
+      const Upstream& up = existing->second.inputs[sinkPort];
+      gsloge("Sink [%s] port [%zu] is already connected to Source [%s] port [%zu]", nameOf(sink), sinkPort,
+             nameOf(up.source), up.port);
+      return Status_InvalidState;
+    }
+    SourceInfo& si = sourceInfo(source);
+    if (si.ports.size() <= sourcePort) si.ports.resize(sourcePort + 1);
+    si.ports[sourcePort].push_back(SinkPortKey{sink, sinkPort});
+
+    SinkInfo& ki = sinkInfo(sink);
+    if (ki.inputs.size() <= sinkPort) ki.inputs.resize(sinkPort + 1);
+    ki.inputs[sinkPort] = Upstream{source, sourcePort};
+
+    if (Sink* s = source->asSink()) mTails.erase(std::remove(mTails.begin(), mTails.end(), s), mTails.end());
+    Source* sinkAsSource = sink->asSource();
+    if ((sinkAsSource == nullptr || mSources.find(sinkAsSource) == mSources.end()) &&
+        std::find(mTails.begin(), mTails.end(), sink) == mTails.end()) {
+      mTails.push_back(sink);
+    }
+    return Status_Success;
+  }
+  IF_CATCH_RETURN_STATUS;
+}
+
+// SteppingDriver.cpp:137-141
+Status SteppingDriver::setupNode(Node* node, const char* functionInGraph) noexcept {
+  if (node == nullptr) return Status_InvalidArgument;
+  try {
+    auto [it, inserted] = mNodes.try_emplace(node, node, functionInGraph);
+    if (inserted) mNodeOrder.push_back(node);
+    else it->second.name = functionInGraph != nullptr ? functionInGraph : "";
+    return Status_Success;
+  }
+  IF_CATCH_RETURN_STATUS;
+}
+
+void SteppingDriver::iterateOverConnections(void* context,
+                                            void (*connectionIterator)(IDriver*, void*, Source*, size_t, Sink*,
+                                                                       size_t) noexcept) noexcept {
+  if (connectionIterator == nullptr) return;
+  for (Source* source : mSourceOrder) {
+    const SourceInfo& si = mSources.at(source);
+    for (size_t p = 0; p < si.ports.size(); ++p)
+      for (const SinkPortKey& k : si.ports[p]) connectionIterator(this, context, source, p, k.sink, k.port);
+  }
+}
+
+void SteppingDriver::iterateOverNodes(void* context, void (*nodeIterator)(IDriver*, void*, Node*) noexcept) noexcept {
+  if (nodeIterator == nullptr) return;
+  for (Node* n : mNodeOrder) nodeIterator(this, context, n);
+}
+
+// The reference keeps no attributes (SteppingDriver.cpp:174-182).
+void SteppingDriver::iterateOverNodeAttributes(Node*, void*,
+                                               void (*)(IDriver*, Node*, void*, const char*, const char*) noexcept)
+    noexcept {}
+
+// SteppingDriver.cpp:465-496: this driver's names first, then nested drivers'.
+size_t SteppingDriver::getNodeName(Node* node, char* name, size_t nameBufLen, bool* foundOut) noexcept {
+  bool found = false;
+  size_t len = 0;
+  auto it = mNodes.find(node);
+  if (it != mNodes.end()) {
+    const std::string& s = it->second.name;
+    len = s.size();
+    if (name != nullptr && nameBufLen > 0) {
+      const size_t n = std::min(len, nameBufLen);
+      std::memcpy(name, s.data(), n);
+      if (nameBufLen > len) name[len] = 0;
+    }
+    found = true;
+  } else {
+    for (Node* n : mNodeOrder) {
+      IDriver* d = n->asDriver();
+      if (d == nullptr || d == this) continue;
+      len = d->getNodeName(node, name, nameBufLen, &found);
+      if (found) break;
+    }
+    if (!found) {
+      len = 0;
+      if (name != nullptr && nameBufLen > 0) name[0] = 0;
+    }
+  }
+  if (foundOut != nullptr) *foundOut = found;
+  return len;
+}
+
+// SteppingDriver.cpp:453-463: every connected output port has bytes to give.
+bool SteppingDriver::hasDataForAllPorts(Source* source) {
+  auto it = mSources.find(source);
+  if (it == mSources.end()) return true;
+  for (size_t p = 0; p < it->second.ports.size(); ++p)
+    if (source->getOutputDataSize(p) == 0) return false;
+  return true;
+}
+
+// SteppingDriver.cpp:193-199
+Status SteppingDriver::doFilter() noexcept {
+  try {
+    for (size_t i = 0; i < mTails.size(); ++i) FWD_IF_ERR(doSinkInput(mTails[i], 0));
+    return Status_Success;
+  }
+  IF_CATCH_RETURN_STATUS;
+}
+
+// SteppingDriver.cpp:201-245: pull every upstream of `sink` (recursing through filters that have
+// no output yet), then move one chunk from each upstream into it. A filter that still has nothing
+// after being fed ends this sink's step.
+Status SteppingDriver::doSinkInput(Sink* sink, int depth) {
+  auto it = mSinks.find(sink);
+  if (it == mSinks.end()) return Status_Success;  // fed from outside this driver
+  if (depth > kMaxDepth) {
+    gsloge("SteppingDriver: upstream chain of [%s] is longer than %d nodes (cycle?)", nameOf(sink), kMaxDepth);
+    return Status_InvalidState;
+  }
+  const size_t nInputs = it->second.inputs.size();
+  for (size_t port = 0; port < nInputs; ++port) {
+    const Upstream up = it->second.inputs[port];
+    if (up.source == nullptr) {
+      gslogt("Sink [%s] port [%zu] does not have a Source connected to it", nameOf(sink), port);
+      continue;
+    }
+    Sink* upstreamSink = up.source->asSink();
+    if (upstreamSink != nullptr && !hasDataForAllPorts(up.source)) {
+      FWD_IF_ERR(doSinkInput(upstreamSink, depth + 1));
+      if (!hasDataForAllPorts(up.source)) return Status_Success;
+    }
+    if (hasDataForAllPorts(up.source)) FWD_IF_ERR(doSourceOutput(up.source));
+  }
+  return Status_Success;
+}
+
+// SteppingDriver.cpp:247-366: each connected sink lends a buffer sized
+// alignUp(min(sink preferred, source available), source alignment); the first sink of a port
+// receives readOutput's data, further sinks of the same port get a copy through the source's
+// output copier; then every sink commits the bytes written.
+Status SteppingDriver::doSourceOutput(Source* source) {
+  SourceInfo& si = mSources.at(source);
+  const size_t nPorts = si.ports.size();
+  for (size_t p = 0; p < nPorts; ++p) {
+    if (si.ports[p].empty()) {
+      gsloge("Source [%s] must have a sink connected to port [%zu]", nameOf(source), p);
+      return Status_InvalidState;
+    }
+  }
+  mBufferRefs.clear();
+  mPortBuffers.assign(nPorts, nullptr);
+  // sinks that lent a buffer, so a failure can cancel their checkout (commit of 0 bytes)
+  auto cancel = [&](size_t lentCount) {
+    size_t i = 0;
+    for (size_t p = 0; p < nPorts && i < lentCount; ++p)
+      for (const SinkPortKey& k : si.ports[p]) {
+        if (i++ >= lentCount) break;
+        (void)k.sink->commitBuffer(k.port, 0);
+      }
+  };
+  for (size_t p = 0; p < nPorts; ++p) {
+    size_t alignment = source->getOutputSizeAlignment(p);
+    if (alignment == 0) alignment = 1;
+    const size_t available = source->getOutputDataSize(p);
+    for (const SinkPortKey& k : si.ports[p]) {
+      const size_t want = std::min(k.sink->preferredInputBufferSize(k.port), available);
+      const size_t bytes = want > SIZE_MAX - alignment + 1 ? want / alignment * alignment
+                                                           : (want + alignment - 1) / alignment * alignment;
+      Result<IBuffer> r = k.sink->requestBuffer(k.port, bytes);
+      if (r.status != Status_Success) {
+        gsloge("Sink [%s] port [%zu] could not lend %zu bytes", nameOf(k.sink), k.port, bytes);
+        cancel(mBufferRefs.size());
+        return r.status;
+      }
+      mBufferRefs.emplace_back(r.value);
+      if (mPortBuffers[p] == nullptr) mPortBuffers[p] = r.value;
+    }
+  }
+  Status st = source->readOutput(mPortBuffers.data(), nPorts);
+  if (st != Status_Success) {
+    gsloge("Source [%s] readOutput failed [%u]", nameOf(source), (unsigned)st);
+    cancel(mBufferRefs.size());
+    return st;
+  }
+  size_t ref = 0;
+  for (size_t p = 0; p < nPorts; ++p) {
+    IBuffer* populated = mPortBuffers[p];
+    const size_t bytes = populated->range()->used();
+    ++ref;  // the populated buffer
+    for (size_t s = 1; s < si.ports[p].size(); ++s, ++ref) {
+      IBuffer* target = mBufferRefs[ref].get();
+      IBufferCopier* copier = source->getOutputCopier(p);
+      if (copier == nullptr) {
+        gsloge("Source [%s] port [%zu] feeds %zu sinks but has no output copier", nameOf(source), p,
+               si.ports[p].size());
+        return Status_InvalidState;
+      }
+      if (target->range()->remaining() < bytes) return Status_OutOfRange;
+      FWD_IF_ERR(copier->copy(target->writePtr(), populated->readPtr(), bytes));
+      FWD_IF_ERR(target->range()->increaseEndOffset(bytes));
+    }
+    for (const SinkPortKey& k : si.ports[p]) FWD_IF_ERR(k.sink->commitBuffer(k.port, bytes));
+  }
+  mBufferRefs.clear();
+  return Status_Success;
+}
+
+}  // namespace gsdr_rt

@@ -1,0 +1,95 @@
+// SteppingDriver: the pull-based caller of the filter graph (reference src/driver/SteppingDriver.cpp,
+// semantics of :102-141 connect/setupNode and :193-366 doFilter/doSinkInput/doSourceOutput).
+//
+// Host-side bookkeeping only; every readOutput() it makes enqueues on the node's own HIP stream.
+// Differences from the reference, all deliberate:
+//  * a sink port records its upstream once (the reference inserts it twice, :121-124);
+//  * graph tails are stepped in connection order (an unordered_set in the reference), so a step is
+//    reproducible;
+//  * node names are looked up only when a message is logged (the reference builds std::string
+//    names on every step, :208-217);
+//  * a cycle in the graph ends the step with Status_InvalidState instead of recursing forever.
+#pragma once
+
+#include <gpusdrpipeline/Factories.h>
+
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace gsdr_rt {
+
+class SteppingDriver final : public ISteppingDriver {
+ public:
+  SteppingDriver() noexcept = default;
+
+  Status connect(Source* source, size_t sourcePort, Sink* sink, size_t sinkPort) noexcept final;
+  Status setupNode(Node* node, const char* functionInGraph) noexcept final;
+  void iterateOverConnections(void* context,
+                              void (*connectionIterator)(IDriver* driver, void* context, Source* source,
+                                                         size_t sourcePort, Sink* sink,
+                                                         size_t sinkPort) noexcept) noexcept final;
+  void iterateOverNodes(void* context,
+                        void (*nodeIterator)(IDriver* driver, void* context, Node* node) noexcept) noexcept final;
+  void iterateOverNodeAttributes(Node* node, void* context,
+                                 void (*nodeAttrIterator)(IDriver* driver, Node* node, void* context,
+                                                          const char* attrName,
+                                                          const char* attrVal) noexcept) noexcept final;
+  size_t getNodeName(Node* node, char* name, size_t nameBufLen, bool* foundOut) noexcept final;
+  Status doFilter() noexcept final;
+
+ private:
+  struct SinkPortKey {
+    Sink* sink;
+    size_t port;
+  };
+  struct Upstream {  // what feeds one sink port
+    Source* source = nullptr;
+    size_t port = 0;
+  };
+  struct SourceInfo {
+    ImmutableRef<Source> source;
+    std::vector<std::vector<SinkPortKey>> ports;  // source port -> connected sink ports, in connect order
+    explicit SourceInfo(Source* s) : source(s) {}
+  };
+  struct SinkInfo {
+    ImmutableRef<Sink> sink;
+    std::vector<Upstream> inputs;  // sink port -> upstream (source == nullptr: unconnected)
+    explicit SinkInfo(Sink* s) : sink(s) {}
+  };
+  struct NodeInfo {
+    ImmutableRef<Node> node;
+    std::string name;
+    NodeInfo(Node* n, const char* nm) : node(n), name(nm != nullptr ? nm : "") {}
+  };
+
+  SourceInfo& sourceInfo(Source* source);
+  SinkInfo& sinkInfo(Sink* sink);
+  const char* nameOf(Node* node) const noexcept;
+  bool hasDataForAllPorts(Source* source);
+  Status doSinkInput(Sink* sink, int depth);
+  Status doSourceOutput(Source* source);
+
+  // std::unordered_map keeps element addresses stable across inserts (references handed out above)
+  std::unordered_map<Source*, SourceInfo> mSources;
+  std::unordered_map<Sink*, SinkInfo> mSinks;
+  std::vector<Source*> mSourceOrder;  // first-connect order, for iterateOverConnections
+  std::vector<Sink*> mTails;          // sinks whose node is not (yet) a connected source
+  std::unordered_map<Node*, NodeInfo> mNodes;
+  std::vector<Node*> mNodeOrder;
+  // per-step scratch, kept to avoid reallocation on every doSourceOutput
+  std::vector<Ref<IBuffer>> mBufferRefs;
+  std::vector<IBuffer*> mPortBuffers;
+
+  REF_COUNTED(SteppingDriver);
+};
+
+class SteppingDriverFactory final : public ISteppingDriverFactory {
+ public:
+  Result<ISteppingDriver> createSteppingDriver() noexcept final {
+    return makeRefResultNonNull<ISteppingDriver>(new (std::nothrow) SteppingDriver());
+  }
+  REF_COUNTED(SteppingDriverFactory);
+};
+
+}  // namespace gsdr_rt

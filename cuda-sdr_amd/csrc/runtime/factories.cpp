@@ -7,6 +7,7 @@
 #include <unordered_map>
 
 #include "buffers.h"
+#include "driver.h"
 #include "filters.h"
 #include "json.h"
 #include "queues.h"
@@ -284,11 +285,6 @@ class StubQueueFilterFactory final : public ICudaFilterFactory {
   const char* mName;
   REF_COUNTED(StubQueueFilterFactory);
 };
-class StubSteppingDriverFactory final : public ISteppingDriverFactory {
- public:
-  Result<ISteppingDriver> createSteppingDriver() noexcept final { GS_OUT_OF_SCOPE("SteppingDriver"); }
-  REF_COUNTED(StubSteppingDriverFactory);
-};
 class StubFilterDriverFactory final : public IFilterDriverFactory {
  public:
   Result<Node> create(const char*) noexcept final { GS_OUT_OF_SCOPE("Component"); }
@@ -353,7 +349,7 @@ class Factories final : public IFactories {
         mFile(new StubFileReaderFactory()),
         mHackrf(new StubHackrfFactory()),
         mMultiply(new StubQueueFilterFactory("MultiplyCCC")),
-        mStepping(new StubSteppingDriverFactory()),
+        mStepping(new SteppingDriverFactory()),
         mComponent(new StubFilterDriverFactory()),
         mRemapSink(new StubPortRemappingSinkFactory()),
         mRemapSource(new StubPortRemappingSourceFactory()),

@@ -56,6 +56,11 @@ def _L():
             "gspBufferSetRange": ([h, sz, sz], u32),
             "gspBufferBase": ([h], vp),
             "gspBufferToHost": ([h, vp, sz, h], u32),
+            "gspSteppingDriverCreate": ([ph], u32),
+            "gspDriverConnect": ([h, h, sz, h, sz], u32),
+            "gspDriverSetupNode": ([h, h, ctypes.c_char_p], u32),
+            "gspDriverDoFilter": ([h], u32),
+            "gspDriverNodeName": ([h, h, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int32)], sz),
         }
         for name, (args, res) in sigs.items():
             fn = getattr(L, name)
@@ -202,3 +207,29 @@ class Node(_Handle):
     def read(self, buffers):
         arr = (ctypes.c_void_p * len(buffers))(*[b.handle.value for b in buffers])
         _check(_L().gspSourceRead(self._h, arr, len(buffers)), "readOutput")
+
+
+class SteppingDriver(_Handle):
+    """ISteppingDriver (reference src/driver/SteppingDriver.cpp): connect nodes, then each
+    ``do_filter()`` pulls one chunk through every graph tail's upstream chain. Holds references
+    to the nodes it connects."""
+
+    def __init__(self):
+        super().__init__(_create(_L().gspSteppingDriverCreate, what="createSteppingDriver"))
+        self._nodes = []
+
+    def connect(self, source: Node, source_port: int, sink: Node, sink_port: int = 0):
+        _check(_L().gspDriverConnect(self._h, source.handle, source_port, sink.handle, sink_port), "connect")
+        self._nodes += [source, sink]
+
+    def setup_node(self, node: Node, name: str):
+        _check(_L().gspDriverSetupNode(self._h, node.handle, name.encode()), "setupNode")
+
+    def node_name(self, node: Node):
+        found = ctypes.c_int32()
+        buf = ctypes.create_string_buffer(256)
+        n = _L().gspDriverNodeName(self._h, node.handle, buf, len(buf), ctypes.byref(found))
+        return buf.raw[:min(n, 255)].decode() if found.value else None
+
+    def do_filter(self):
+        _check(_L().gspDriverDoFilter(self._h), "doFilter")

@@ -72,6 +72,17 @@ GSP_API void* gspBufferBase(gspHandle buffer);
 /* Copies the buffer's used bytes (at most `bytes`) to host and synchronises the queue. */
 GSP_API uint32_t gspBufferToHost(gspHandle buffer, void* host, size_t bytes, gspHandle queue);
 
+/* SteppingDriver (ISteppingDriver, SteppingDriver.cpp:102-366): connect nodes, name them, and
+ * pull one step of every graph tail. Handles are nodes from the creators above. */
+GSP_API uint32_t gspSteppingDriverCreate(gspHandle* driverOut);
+GSP_API uint32_t gspDriverConnect(gspHandle driver, gspHandle source, size_t sourcePort, gspHandle sink,
+                                  size_t sinkPort);
+GSP_API uint32_t gspDriverSetupNode(gspHandle driver, gspHandle node, const char* name);
+GSP_API uint32_t gspDriverDoFilter(gspHandle driver);
+/* Name given to `node` by setupNode (this driver or a nested one); *found = 0 if none. Returns the
+ * name length; at most nameBufLen bytes are written (NUL-terminated when it fits). */
+GSP_API size_t gspDriverNodeName(gspHandle driver, gspHandle node, char* name, size_t nameBufLen, int32_t* found);
+
 #ifdef __cplusplus
 }
 #endif

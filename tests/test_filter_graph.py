@@ -135,3 +135,44 @@ def test_json_nodes_and_out_of_scope(graph, queue):
         graph.Node.from_json("Fir", "{broken")
     assert e.value.status == 9  # Status_ParseError
     del lib, ctypes
+
+
+@pytest.mark.parametrize("T,D", [(127, 1), (127, 3), (1023, 10)])
+def test_stepping_driver_am_chain(graph, queue, orc, T, D):
+    """Int8ToFloat -> Fir -> QuadAmDemod stepped by the SteppingDriver (SteppingDriver.cpp:193-366):
+    the head is fed from outside the driver, every doFilter pulls one chunk through the chain, and
+    the AM tail is drained between steps; the concatenated output equals the oracle chain over the
+    whole stream (count rule Fir.cpp:178-186)."""
+    rng = np.random.default_rng(T + D)
+    taps = orc.lowpass_taps(T, 0.4 / D)
+    conv = graph.Node.int8_to_float(queue)
+    fir = graph.Node.fir(queue, taps, D, graph.SAMPLE_FLOAT_COMPLEX)
+    am = graph.Node.quad_am_demod(queue)
+    drv = graph.SteppingDriver()
+    drv.connect(fir, 0, am, 0)  # downstream first: the tail must still be the AM node
+    drv.connect(conv, 0, fir, 0)
+    for node, name in ((conv, "int8ToFloat"), (fir, "fir"), (am, "amDemod")):
+        drv.setup_node(node, name)
+    assert drv.node_name(fir) == "fir"
+    model = orc.FirStreamModel(taps, D)
+    got, want, bounds = [], [], []
+    for step in range(12):
+        n = int(rng.integers(1, 200_000))
+        iq = rng.integers(-128, 128, size=2 * n).astype(np.int8)
+        conv.push(iq)
+        model.push(orc.int8_to_float(iq).view(np.complex64))
+        expect = model.output_count()
+        for _ in range(64):  # a step moves at most the preferred 1 MiB per edge
+            if am.output_size()[0] >= 4 * expect:
+                break
+            drv.do_filter()
+        size, _ = am.output_size()
+        assert size == 4 * expect
+        got.append(_drain(graph, queue, am, max(size, 4), np.float32))
+        y64, bound = model.read(model.output_count())
+        want.append(np.abs(y64))
+        bounds.append(bound)
+    got, want, bound = np.concatenate(got), np.concatenate(want), np.concatenate(bounds)
+    assert len(got) == len(want) > 0
+    # AM of an FIR output: the FIR bound plus the sqrt rounding (AM_TOL relative)
+    assert np.all(np.abs(got - want) <= FIR_TOL * bound + 1e-6 * want + 1e-30)
