@@ -19,7 +19,10 @@ halo <- g-1, RCCL over xGMI), overlapped with the bulk kernel that needs no halo
 head kernel finishes the first T-1 outputs once the halo has landed.
 
 Other workloads (--workload): c3 (cf32 2^28, 1023 taps, D=10, FIR->AM), c4 (cf32, 1023 taps,
-D=1, FIR->AM).
+D=1, FIR->AM), c5 (the full AM receive chain int8 IQ -> 1023-tap FIR, D=10 -> AM -> 255-tap audio
+FIR, D=20 through the gsdrAmChain executor: one hipGraph launch per 5 M-sample chunk, 1 s of a
+1 Gsps stream split over 8 GPUs = 125 M samples per GPU step; ranks own disjoint time ranges and
+are primed by the warm-up steps, so no data-path collective).
 
 Output: one JSON line on rank 0 (contract in the task statement) with `roofline` for the
 dominant kernel (HIP events on its stream) and `cpu_baseline` (oracle port, rank 0, N=1).
@@ -52,7 +55,12 @@ WORKLOADS = {
            "c64", (1 << 28) - (1 << 28) % 10, 1023, 10, 0.04, "blackman", 200e6),
     "c4": ("C4: cf32 stream, 1023-tap FC FIR, D=1 -> QuadAmDemod, 2^26 samples per GPU step",
            "c64", 1 << 26, 1023, 1, 0.04, "blackman", 1e9),
+    "c5": ("C5: full AM chain @1 Gsps (1/8 per GPU): int8 IQ -> 1023-tap FC FIR, D=10 -> AM -> 255-tap FF "
+           "FIR, D=20, 125 M samples (1 s) per GPU step, hipGraph-captured",
+           "i8", 125_000_000, 1023, 10, 0.04, "blackman", 1e9),
 }
+C5_CHUNK = 5_000_000   # multiple of D * Da = 200
+C5_AUDIO = (255, 20, 0.02, "hamming")
 
 
 def lowpass(num_taps, cutoff, window):
@@ -168,6 +176,56 @@ class ShardedChain:
         return self.kind == "c64" and self.T >= 64 and self.D <= 16 and 31 * self.D + self.T <= 1408
 
 
+class AmChainRunner:
+    """C5: the gsdrAmChain executor (one hipGraph per chunk) over a resident 1-second segment.
+
+    Each rank owns its own time range of the synthetic 1 Gsps stream (rank g starts at g * L);
+    the chain history carries across steps, and the warm-up steps prime it, so the timed steps are
+    all steady-state (no data-path collective; weak scaling)."""
+
+    def __init__(self, ops, rank, world, device, mode="resident"):
+        from gpusdr.chain import AmChain
+        desc, kind, L, T, D, cutoff, window, fs = WORKLOADS["c5"]
+        Ta, Da, cut_a, win_a = C5_AUDIO
+        self.kind, self.L, self.T, self.D, self.Ta, self.Da = kind, L, T, D, Ta, Da
+        self.mode = mode
+        self.chunks = L // C5_CHUNK
+        assert self.chunks * C5_CHUNK == L
+        self.chain = AmChain(lowpass(T, cutoff, window), D, lowpass(Ta, cut_a, win_a), Da, C5_CHUNK, device.index)
+        # [RF history | 1 s segment]: resident steps read the history in place in front of it
+        self.hist = 2 * 2048
+        self.buf = torch.empty(self.hist + 2 * L, dtype=torch.int8, device=device)
+        ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, rank * L, L + self.hist // 2, out=self.buf)
+        self.iq = self.buf[self.hist:]
+        self.out = torch.empty(L // (D * Da) + C5_CHUNK, dtype=torch.float32, device=device)
+        self.stream = self.chain.torch_stream
+        self.geom = None
+        self.single = world == 1
+        self.mfma_int8 = self.mfma_cf = False
+
+    def step(self, ev=None):
+        with torch.cuda.stream(self.stream):
+            if ev is not None:
+                ev[0].record(self.stream)
+            if self.mode == "resident":
+                self.chain.step_resident(self.iq, self.chunks, self.out)
+            else:
+                n = C5_CHUNK // (self.D * self.Da)
+                pos = 0
+                for c in range(self.chunks):
+                    got = self.chain.step(self.iq[2 * C5_CHUNK * c: 2 * C5_CHUNK * (c + 1)], self.out[pos: pos + n])
+                    pos += got.numel()
+            if ev is not None:
+                ev[1].record(self.stream)
+
+    def timed_bytes_ops(self):
+        """Per timed region (all chunks of a step): int8 input read once + audio written once;
+        direct-form flops of both FIRs (4 T / D per input sample, 2 Ta / Da per AM sample)."""
+        n_rf = self.L // self.D
+        n_audio = n_rf // self.Da
+        return 2 * self.L + 4 * n_audio, n_rf * self.T * 4 + n_audio * self.Ta * 2
+
+
 def cpu_baseline(wl, seconds_target=8.0):
     """Oracle port (float32 direct form, all assigned host cores) on a bounded sample."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -202,11 +260,15 @@ def cpu_baseline(wl, seconds_target=8.0):
         "cores": threads,
         "kind": "port",
         "sample": f"{n_out * D} input samples of the {wl} chain (oracle/gsdr_oracle.c float32 direct form, "
-                  f"{threads} threads, mean of {reps} runs)",
+                  f"{threads} threads, mean of {reps} runs"
+                  + ("; RF FIR + AM only, the audio FIR is 0.6 % of the flops)" if wl == "c5" else ")"),
     }
 
 
 def kernel_name(chain):
+    if isinstance(chain, AmChainRunner):
+        return (f"gsdrAmChain {chain.mode} step graph (firI8DecMfmaKernel RF FIR+AM, audio FIR, history copies; "
+                "HIP events around the whole step)")
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"
     body = "firI8MfmaKernel" if chain.mfma_int8 else ("firCfMfmaKernel" if chain.mfma_cf else "firLdsKernel")
@@ -231,12 +293,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c5-mode", default="resident", choices=["resident", "chunked"],
+                    help="c5: one graph over the resident 1 s segment, or one graph per 5 M-sample chunk")
     args = ap.parse_args()
 
     rank, world, local = dist_setup(args.gpus)
     device = torch.device("cuda", local)
     from gpusdr import ops
-    chain = ShardedChain(ops, args.workload, rank, world, device)
+    chain = AmChainRunner(ops, rank, world, device, args.c5_mode) if args.workload == "c5" else \
+        ShardedChain(ops, args.workload, rank, world, device)
 
     for _ in range(args.warmup):
         chain.step()
@@ -290,8 +355,12 @@ def main():
                 "taps": chain.T,
                 "decimation": chain.D,
                 "input": "int8 IQ" if chain.kind == "i8" else "cf32",
-                "parallelism": f"time-shard x{world} (ring halo of {chain.geom.halo} samples over RCCL)"
+                "parallelism": ("disjoint time ranges per rank, history primed by warm-up (no collective)"
+                                if chain.geom is None else
+                                f"time-shard x{world} (ring halo of {chain.geom.halo} samples over RCCL)")
                 if world > 1 else "single GPU (halo = own history carry)",
+                **({"c5_mode": chain.mode, "chunk_samples": C5_CHUNK, "audio_taps": chain.Ta,
+                    "audio_decimation": chain.Da} if isinstance(chain, AmChainRunner) else {}),
             },
             "roofline": {
                 "bound": "hbm",

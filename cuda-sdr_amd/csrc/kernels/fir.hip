@@ -347,6 +347,118 @@ __global__ __launch_bounds__(kThreads) void firDirectKernel(FirArgs a) {
   }
 }
 
+// Small launches (fewer LDS-kernel tiles than CUs) and many-phase FF (the C5 audio FIR, D = 20):
+// one output per thread over a 256-output block whose input window (255 D + T samples) is staged
+// in LDS PHASE-MAJOR (x_p[m] = x[m D + p] at p M + m), so the 64 lanes of a tap step read 64
+// consecutive words - no bank conflicts at any D - and the taps, staged phase-major too, are LDS
+// broadcasts. Sum: 64-tap partials per phase, added in order (a different grouping than
+// firLdsKernel's; the tests bound both against float64).
+template <int INK>
+struct SmallElem;
+template <>
+struct SmallElem<kInF32> {
+  typedef float T;
+};
+template <>
+struct SmallElem<kInCF32> {
+  typedef f2 T;
+};
+template <>
+struct SmallElem<kInI8IQ> {
+  typedef char2 T;
+};
+
+// rows per phase region: the block's 256 outputs + the phase's taps, odd (spreads the staging
+// writes over the banks)
+__host__ __device__ inline int smallRows(int T, int D) { return (kThreads + (T + D - 1) / D) | 1; }
+
+template <int MODE, int INK, int EPI>
+__global__ __launch_bounds__(kThreads) void firSmallKernel(FirArgs a) {
+  typedef typename SmallElem<INK>::T E;
+  constexpr int kTapF = (MODE == kFirCC || MODE == kFirCF) ? 2 : 1;  // floats per tap
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int D = a.D, T = a.T;
+  const int M = smallRows(T, D);
+  const int deff = D < T ? D : T;  // phases holding taps (D > T: the others are never read)
+  const int qmax = (T + D - 1) / D;
+  float* tapsL = reinterpret_cast<float*>(smem);  // phase-major: tap (p, q) at p qmax + q
+  E* win = reinterpret_cast<E*>(smem + ((size_t)(kTapF * 4 * deff * qmax + 15) & ~(size_t)15));
+  const int64_t k0 = (int64_t)blockIdx.x * kThreads;
+  const int64_t base = k0 * D;
+  const int64_t avail = a.nIn - base;
+  const int64_t span = (int64_t)(kThreads - 1) * D + T;
+  const int nWin = (int)(avail < span ? avail : span);
+  const E* src = reinterpret_cast<const E*>(a.in) + base;
+  // staging: 8 independent loads in flight per thread before the scattered LDS stores (a plain
+  // loop waits out the HBM latency once per element); i / D through a float reciprocal, corrected
+  const float invD = 1.0f / (float)D;
+  for (int i0 = 0; i0 < nWin; i0 += 8 * kThreads) {
+    E v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * kThreads + (int)threadIdx.x;
+      v[u] = src[i < nWin ? i : nWin - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * kThreads + (int)threadIdx.x;
+      int m = (int)((float)i * invD);
+      m -= m * D > i ? 1 : 0;
+      m += (m + 1) * D <= i ? 1 : 0;
+      const int p = i - m * D;
+      if (i < nWin && p < deff) win[p * M + m] = v[u];
+    }
+  }
+  for (int j = threadIdx.x; j < T; j += kThreads) {
+    const int q = j / D;
+    const int p = j - q * D;
+#pragma unroll
+    for (int c = 0; c < kTapF; ++c) tapsL[kTapF * (p * qmax + q) + c] = a.taps[kTapF * j + c];
+  }
+  __syncthreads();
+  const int64_t k = k0 + threadIdx.x;
+  if (k >= a.nOut) return;
+  f2 tot = {0.0f, 0.0f};
+  for (int p = 0; p < deff; ++p) {
+    const E* x = win + p * M + threadIdx.x;
+    const float* h = tapsL + kTapF * p * qmax;
+    const int qn = (T - p + D - 1) / D;
+    for (int qb = 0; qb < qn; qb += 64) {  // blocked sum: 64-tap partials, error ~ (64 + T / 64) eps
+      const int qe = qn - qb < 64 ? qn : qb + 64;
+      f2 acc = {0.0f, 0.0f};
+#pragma unroll 8
+      for (int q = qb; q < qe; ++q) {
+        f2 z;
+        if constexpr (INK == kInCF32) {
+          z = x[q];
+        } else if constexpr (INK == kInI8IQ) {
+          const char2 v = x[q];
+          z = f2{int8ToNorm(v.x), int8ToNorm(v.y)};
+        } else {
+          z = f2{x[q], x[q]};
+        }
+        if (MODE == kFirFF || MODE == kFirFC) {
+          acc = __builtin_elementwise_fma(f2{h[q], h[q]}, z, acc);
+        } else if (MODE == kFirCF) {
+          acc = __builtin_elementwise_fma(f2{h[2 * q], h[2 * q + 1]}, z, acc);
+        } else {
+          const float hr = h[2 * q], hi = h[2 * q + 1];
+          acc = __builtin_elementwise_fma(f2{hr, hr}, z, acc);
+          acc = __builtin_elementwise_fma(f2{-hi, hi}, f2{z.y, z.x}, acc);
+        }
+      }
+      tot += acc;
+    }
+  }
+  if (EPI == kEpiComplex) {
+    reinterpret_cast<f2*>(a.out)[k] = tot;
+  } else if (EPI == kEpiAm) {
+    reinterpret_cast<float*>(a.out)[k] = amEnvelope(tot);
+  } else {
+    reinterpret_cast<float*>(a.out)[k] = tot.x;
+  }
+}
+
 // ---- host side --------------------------------------------------------------------------
 
 namespace {
@@ -433,6 +545,9 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
   if constexpr (MODE == kFirFC && INK == kInI8IQ && EPI != kEpiPair) {
     if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firI8MfmaEligible(tapCount, decimation, in))
       return launchFirI8Mfma(static_cast<const int8_t*>(in), taps, tapCount, out, nOut, EPI, stream);
+    // decimating / long filters: the split-K Toeplitz kernel on f16 planes
+    if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firI8DecMfmaEligible(tapCount, decimation, in))
+      return launchFirI8DecMfma(static_cast<const int8_t*>(in), taps, tapCount, decimation, out, nOut, EPI, stream);
   }
   // cf32 with real taps: the split-precision bf16 MFMA kernel for the long-filter shapes
   if constexpr (MODE == kFirFC && INK == kInCF32 && EPI != kEpiPair) {
@@ -457,6 +572,27 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
     const int64_t blocks = ((int64_t)nOut + kThreads - 1) / kThreads;
     hipLaunchKernelGGL((firDirectKernel<MODE, INK, EPI>), dim3((unsigned)blocks), dim3(kThreads), 0, stream, a);
     return hipGetLastError();
+  }
+  // small launches: the LDS-kernel grid would leave most CUs idle
+  {
+    const int64_t perTile = (int64_t)s.tileOutputs * (MODE == kFirFF ? 2 : 1);
+    const int64_t tiles = ((int64_t)nOut + perTile - 1) / perTile;
+    const size_t elem = INK == kInF32 ? 4 : (INK == kInCF32 ? 8 : 2);
+    const size_t deff = s.decimation < tapCount ? s.decimation : tapCount;
+    const size_t qmax = (tapCount + s.decimation - 1) / s.decimation;
+    const size_t tapBytes = ((MODE == kFirCC || MODE == kFirCF) ? 8 : 4) * deff * qmax;
+    const size_t lds = ((tapBytes + 15) & ~(size_t)15) + elem * (size_t)smallRows((int)tapCount, (int)s.decimation) * deff;
+    // FF with many phases (the C5 audio FIR, D = 20): the phase-major staging of the LDS kernel
+    // costs more than the taps; one output per thread over a shared window is faster
+    const bool manyPhasesFF = MODE == kFirFF && s.decimation >= 8;
+    if ((tiles < 128 || manyPhasesFF) && lds <= kLdsSoftLimit) {
+      auto kernel = firSmallKernel<MODE, INK, EPI>;
+      hipError_t e = ensureLds(kernel, lds);
+      if (e != hipSuccess) return e;
+      const int64_t blocks = ((int64_t)nOut + kThreads - 1) / kThreads;
+      hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kThreads), lds, stream, a);
+      return hipGetLastError();
+    }
   }
   a.regionRows = (int32_t)s.regionRows;
   a.tileOutputs = (int32_t)s.tileOutputs;

@@ -23,6 +23,13 @@
 // Plane units (8 samples, 16 B) are padded (unit u at u + (u >> padShift)) and the I / Q planes
 // offset so that every ds_read_b128 lane group of the A fragments is bank-conflict free; the host
 // picks both per D (cfPlaneLayout).
+//
+// int8 IQ input (firI8DecMfmaKernel: gsdrInt8FirFC / gsdrInt8FirFCAmDemod with D > 1 or T > 129,
+// the C5 RF stage; any sample-aligned input): the same Toeplitz tiles and work split, but
+// x' = max(x, -127) is an integer,
+// exact in f16, so the window becomes two f16 planes (I, Q) with one split pass of 3 VALU per
+// sample pair, and the taps are scaled by a block-uniform 2^sc and split into two f16 limbs as in
+// fir_i8_mfma.hip: 2 v_mfma_f32_32x32x16_f16 per K-step instead of 6 bf16 products.
 #include <mutex>
 
 #include "kcommon.h"
@@ -271,6 +278,177 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
   }
 }
 
+
+// ---- int8 IQ input -------------------------------------------------------------------------
+
+struct I8DecArgs {
+  const int8_t* iq4;  // the input rounded down to 4 bytes; the samples start `sub` bytes later
+  const float* taps;
+  void* out;
+  int64_t nOut;
+  int64_t nIn;        // complex samples readable: (nOut - 1) D + T
+  int32_t sub;        // 0 or 2: byte offset of the first sample inside its dword
+  int32_t T;
+  int32_t D;
+  int32_t KS;
+  int32_t tiles;
+  int32_t Wu;         // window units (8 samples = 16 input bytes) per tile = 60 D + 16 KS
+  int32_t padShift;
+  int32_t planeStride;  // bytes between the I and Q f16 planes
+};
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+template <int G>
+struct I8DecWindow {
+  uint32_t d[G][5];  // the dword holding the unit's first byte and the next four (a 2-byte-aligned
+                     // unit straddles five)
+};
+
+// Branch-free window loads (kept in flight until the split), one dword each: indices are clamped
+// to the last dword holding input bytes, which never crosses a page; clamped data only meets zero
+// taps or feeds outputs >= nOut. (A dwordx4 clamped as a whole would shift the valid dwords of
+// the input's last unit.)
+template <int G>
+__device__ __forceinline__ void loadWindowI8(const I8DecArgs& a, int tile, int tid, I8DecWindow<G>& w) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(a.iq4);
+  const int64_t base = (int64_t)tile * kCfTileOut * a.D / 2;  // dwords (tile starts: multiples of 8 samples)
+  const int64_t lastDw = (2 * a.nIn - 1 + a.sub) >> 2;
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int g = min(tid + kCfThreads * j, a.Wu - 1);
+    const int64_t i = base + 4 * (int64_t)g;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) w.d[j][q] = d[i + q < lastDw ? i + q : lastDw];
+  }
+}
+
+template <int G>
+__device__ __forceinline__ void splitWindowI8(const I8DecArgs& a, const I8DecWindow<G>& w, int8_t* planes, int tid) {
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int g = tid + kCfThreads * j;
+    if (g < a.Wu) {
+      uint32_t words[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) words[q] = __builtin_amdgcn_alignbyte(w.d[j][q + 1], w.d[j][q], a.sub);
+      uint4 iu, qu;
+      int8IqToF16Units(words, iu, qu);
+      const int off = 16 * cfPhys(g, a.padShift);
+      *reinterpret_cast<uint4*>(planes + off) = iu;
+      *reinterpret_cast<uint4*>(planes + a.planeStride + off) = qu;
+    }
+  }
+}
+
+template <int KS, int G, int EPI>
+__global__ __launch_bounds__(kCfThreads, 1) void firI8DecMfmaKernel(I8DecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  int8_t* planes = smem;
+  float* part = reinterpret_cast<float*>(smem + 2 * a.planeStride);
+  __shared__ float waveMax[kCfWaves];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int D = a.D, T = a.T;
+
+  const int q = a.tiles / (int)gridDim.x, r = a.tiles % (int)gridDim.x;
+  const int t0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
+  const int n = q + ((int)blockIdx.x < r ? 1 : 0);
+  if (n <= 0) return;
+
+  I8DecWindow<G> win;
+  loadWindowI8<G>(a, t0, tid, win);
+
+  // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), block max, two f16 limbs per tap ----------
+  const int off0 = 31 * D;
+  const int span = off0 + 128 * KS;
+  float m = 0.0f;
+  for (int i = tid; i < span; i += kCfThreads) {
+    const int j = i - off0;
+    const float h = (j >= 0 && j < T) ? a.taps[j] : 0.0f;
+    part[i] = h;
+    m = fmaxf(m, fabsf(h));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (lane == 0) waveMax[wave] = m;
+  __syncthreads();
+  float maxAbs = waveMax[0];
+#pragma unroll
+  for (int v = 1; v < kCfWaves; ++v) maxAbs = fmaxf(maxAbs, waveMax[v]);
+  const int sc = maxAbs > 0.0f ? 14 - ilogbf(maxAbs) : 0;  // max |h 2^sc| in [2^14, 2^15)
+  const float outScale = ldexpf(1.0f / 127.0f, -sc);
+  const int half = lane >> 5;
+  const int col = lane & 31;
+  h8 bh[kCfMaxKS], bl[kCfMaxKS];
+#pragma unroll
+  for (int s = 0; s < kCfMaxKS; ++s) {
+    if (s < KS) {
+      const int kap = 16 * (wave * KS + s) + 8 * half;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float hs = ldexpf(part[off0 + kap + e - col * D], sc);
+        const _Float16 hi = (_Float16)hs;
+        bh[s][e] = hi;
+        bl[s][e] = (_Float16)(hs - (float)hi);
+      }
+    } else {
+      bh[s] = h8{};
+      bl[s] = h8{};
+    }
+  }
+  __syncthreads();  // the tap staging area becomes the partial-sum area
+
+  splitWindowI8<G>(a, win, planes, tid);
+  if (n > 1) loadWindowI8<G>(a, t0 + 1, tid, win);
+  __syncthreads();
+
+  const int arow = lane & 15;
+  const int comp = (lane >> 4) & 1;
+  const int uRow = 4 * D * arow + half;
+  const int8_t* pI = planes + comp * a.planeStride;
+
+  for (int i = 0; i < n; ++i) {
+    const int tile = t0 + i;
+    v16f acc = v16f{};
+#pragma unroll
+    for (int s = 0; s < kCfMaxKS; ++s) {
+      if (s < KS) {
+        const int u = uRow + 2 * (wave * KS + s);
+        const h8 x = *reinterpret_cast<const h8*>(pI + 16 * cfPhys(u, a.padShift));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x, bh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x, bl[s], acc, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
+    __syncthreads();  // partials complete; every wave is done reading the planes
+
+    float yi = 0.0f, yq = 0.0f;
+#pragma unroll
+    for (int v = 0; v < kCfWaves; ++v) {
+      yi += part[(v * 16 + wave) * kWave + lane];
+      yq += part[(v * 16 + wave + 8) * kWave + lane];
+    }
+    const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * half;
+    const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
+    if (k < a.nOut) {
+      if (EPI == kEpiAm) {
+        reinterpret_cast<float*>(a.out)[k] = __builtin_amdgcn_sqrtf(fmaf(yi, yi, yq * yq)) * outScale;
+      } else {
+        reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
+      }
+    }
+
+    if (i + 1 < n) {
+      splitWindowI8<G>(a, win, planes, tid);
+      if (i + 2 < n) loadWindowI8<G>(a, tile + 2, tid, win);
+      __syncthreads();
+    }
+  }
+}
+
 // ---- host side ------------------------------------------------------------------------------
 
 namespace {
@@ -289,7 +467,7 @@ struct CfLayout {
 
 // Pick the plane padding and the I/Q plane offset that minimise the A-fragment bank conflicts
 // for this (D, KS), within the LDS budget.
-CfLayout cfPlaneLayout(int D, int KS, int Wu) {
+CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes) {
   CfLayout best{4, 0};
   double bestCost = 1e30;
   for (int p = 4; p >= 1; --p) {
@@ -297,7 +475,7 @@ CfLayout cfPlaneLayout(int D, int KS, int Wu) {
     const int base = (16 * units + 255) / 256 * 256;
     for (int qoff = 0; qoff < 16; ++qoff) {
       const int stride = base + 16 * qoff;
-      if (6 * stride + kCfPartialBytes > kCfDynLdsMax) continue;
+      if (nPlanes * stride + kCfPartialBytes > kCfDynLdsMax) continue;
       double cost = 0;
       for (int s = 0; s < kCfWaves * KS; ++s) {
         for (const auto& grp : kB128Groups) {
@@ -317,7 +495,7 @@ CfLayout cfPlaneLayout(int D, int KS, int Wu) {
           cost += worst;
         }
       }
-      cost += 1e-3 * (6.0 * stride) / 1024.0;  // tie-break: less LDS
+      cost += 1e-3 * (nPlanes * (double)stride) / 1024.0;  // tie-break: less LDS
       if (cost < bestCost) {
         bestCost = cost;
         best = CfLayout{p, stride};
@@ -347,6 +525,30 @@ hipError_t launchCfKS(const CfFirArgs& a, size_t lds, int grid, int epi, hipStre
     case 1: return epi == kEpiAm ? launchCfG<KS, 1, kEpiAm>(a, lds, grid, stream) : launchCfG<KS, 1, kEpiComplex>(a, lds, grid, stream);
     case 2: return epi == kEpiAm ? launchCfG<KS, 2, kEpiAm>(a, lds, grid, stream) : launchCfG<KS, 2, kEpiComplex>(a, lds, grid, stream);
     default: return epi == kEpiAm ? launchCfG<KS, 3, kEpiAm>(a, lds, grid, stream) : launchCfG<KS, 3, kEpiComplex>(a, lds, grid, stream);
+  }
+}
+
+
+template <int KS, int G, int EPI>
+hipError_t launchI8DecG(const I8DecArgs& a, size_t lds, int grid, hipStream_t stream) {
+  static std::once_flag once;
+  static hipError_t attrErr = hipSuccess;
+  std::call_once(once, [] {
+    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(&firI8DecMfmaKernel<KS, G, EPI>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kCfDynLdsMax);
+  });
+  if (attrErr != hipSuccess) return attrErr;
+  hipLaunchKernelGGL((firI8DecMfmaKernel<KS, G, EPI>), dim3(grid), dim3(kCfThreads), lds, stream, a);
+  return hipGetLastError();
+}
+
+template <int KS>
+hipError_t launchI8DecKS(const I8DecArgs& a, size_t lds, int grid, int epi, hipStream_t stream) {
+  const int G = (a.Wu + kCfThreads - 1) / kCfThreads;
+  switch (G) {
+    case 1: return epi == kEpiAm ? launchI8DecG<KS, 1, kEpiAm>(a, lds, grid, stream) : launchI8DecG<KS, 1, kEpiComplex>(a, lds, grid, stream);
+    case 2: return epi == kEpiAm ? launchI8DecG<KS, 2, kEpiAm>(a, lds, grid, stream) : launchI8DecG<KS, 2, kEpiComplex>(a, lds, grid, stream);
+    default: return epi == kEpiAm ? launchI8DecG<KS, 3, kEpiAm>(a, lds, grid, stream) : launchI8DecG<KS, 3, kEpiComplex>(a, lds, grid, stream);
   }
 }
 
@@ -380,7 +582,7 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
   {
     std::lock_guard<std::mutex> lock(mu);
     if (cachedD != a.D || cachedKS != a.KS) {
-      cached = cfPlaneLayout(a.D, a.KS, a.Wu);
+      cached = cfPlaneLayout(a.D, a.KS, a.Wu, 6);
       cachedD = a.D;
       cachedKS = a.KS;
     }
@@ -402,6 +604,61 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
     case 9: return launchCfKS<9>(a, lds, grid, epi, stream);
     case 10: return launchCfKS<10>(a, lds, grid, epi, stream);
     default: return launchCfKS<11>(a, lds, grid, epi, stream);
+  }
+}
+
+bool firI8DecMfmaEligible(size_t tapCount, size_t decimation, const void* in) {
+  const size_t d = decimation < 1 ? 1 : decimation;
+  // the Toeplitz K = 31 D + T beats the fp32 direct form once T >= 5 D (16x the FLOP rate, 2 limbs)
+  return tapCount >= 32 && tapCount >= 5 * d && d <= (size_t)kCfMaxD &&
+         31 * d + tapCount <= (size_t)(kCfWaves * kCfMaxKS * 16) && (reinterpret_cast<uintptr_t>(in) & 1u) == 0;
+}
+
+hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCount, size_t decimation, void* out,
+                              size_t nOut, int epi, hipStream_t stream) {
+  I8DecArgs a{};
+  a.sub = (int32_t)(reinterpret_cast<uintptr_t>(iq) & 3u);
+  a.iq4 = iq - a.sub;
+  a.taps = taps;
+  a.out = out;
+  a.D = (int32_t)(decimation < 1 ? 1 : decimation);
+  a.T = (int32_t)tapCount;
+  a.nOut = (int64_t)nOut;
+  a.nIn = (int64_t)(nOut - 1) * a.D + (int64_t)tapCount;
+  const int ksteps = (31 * a.D + a.T + 15) / 16;
+  a.KS = (ksteps + kCfWaves - 1) / kCfWaves;
+  const int64_t tiles = ((int64_t)nOut + kCfTileOut - 1) / kCfTileOut;
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  a.tiles = (int32_t)tiles;
+  a.Wu = 60 * a.D + 16 * a.KS;
+  static std::mutex mu;
+  static int cachedD = -1, cachedKS = -1;
+  static CfLayout cached{};
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    if (cachedD != a.D || cachedKS != a.KS) {
+      cached = cfPlaneLayout(a.D, a.KS, a.Wu, 2);
+      cachedD = a.D;
+      cachedKS = a.KS;
+    }
+    a.padShift = cached.padShift;
+    a.planeStride = cached.planeStride;
+  }
+  const size_t lds = 2 * (size_t)a.planeStride + kCfPartialBytes;
+  if (a.planeStride == 0 || lds > (size_t)kCfDynLdsMax) return hipErrorInvalidValue;
+  const int grid = (int)(tiles < 256 ? tiles : 256);
+  switch (a.KS) {
+    case 1: return launchI8DecKS<1>(a, lds, grid, epi, stream);
+    case 2: return launchI8DecKS<2>(a, lds, grid, epi, stream);
+    case 3: return launchI8DecKS<3>(a, lds, grid, epi, stream);
+    case 4: return launchI8DecKS<4>(a, lds, grid, epi, stream);
+    case 5: return launchI8DecKS<5>(a, lds, grid, epi, stream);
+    case 6: return launchI8DecKS<6>(a, lds, grid, epi, stream);
+    case 7: return launchI8DecKS<7>(a, lds, grid, epi, stream);
+    case 8: return launchI8DecKS<8>(a, lds, grid, epi, stream);
+    case 9: return launchI8DecKS<9>(a, lds, grid, epi, stream);
+    case 10: return launchI8DecKS<10>(a, lds, grid, epi, stream);
+    default: return launchI8DecKS<11>(a, lds, grid, epi, stream);
   }
 }
 

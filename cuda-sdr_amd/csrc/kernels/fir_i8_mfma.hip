@@ -42,7 +42,6 @@
 namespace gsdr_amd {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int kI8Waves = 4;
@@ -168,29 +167,6 @@ __device__ __forceinline__ void issueChunk(uintptr_t alignedBase, uintptr_t last
   }
 }
 
-// Four interleaved IQ words (I0 Q0 I1 Q1 each) -> clamped f16 I and Q units (8 samples each).
-// u = x ^ 0x80 = x + 128 lands in the low byte of the f16 1024 + u (high byte 0x64); adding
-// -1152 gives x exactly, and max(., -127) is the reference's fmaxf(-1, x/127) clamp.
-__device__ __forceinline__ void splitWords(const uint32_t (&w)[4], uint4& iu, uint4& qu) {
-  const h2 bias = {(_Float16)-1152.0f, (_Float16)-1152.0f};
-  const h2 lo = {(_Float16)-127.0f, (_Float16)-127.0f};
-  uint32_t ri[4], rq[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t u = w[q] ^ 0x80808080u;
-    const uint32_t pi = __builtin_amdgcn_perm(0x64646464u, u, 0x04020400u);
-    const uint32_t pq = __builtin_amdgcn_perm(0x64646464u, u, 0x04030401u);
-    h2 fi = __builtin_bit_cast(h2, pi) + bias;
-    h2 fq = __builtin_bit_cast(h2, pq) + bias;
-    fi = __builtin_elementwise_max(fi, lo);
-    fq = __builtin_elementwise_max(fq, lo);
-    ri[q] = __builtin_bit_cast(uint32_t, fi);
-    rq[q] = __builtin_bit_cast(uint32_t, fq);
-  }
-  iu = uint4{ri[0], ri[1], ri[2], ri[3]};
-  qu = uint4{rq[0], rq[1], rq[2], rq[3]};
-}
-
 // Split one landed slot into the f16 I / Q planes: group g = samples [8g, 8g + 8) of the window
 // at window bytes [16 g, 16 g + 16); `win` is 4-byte aligned when sub = 0, else 2-byte aligned.
 template <int S>
@@ -213,7 +189,7 @@ __device__ __forceinline__ void splitSlot(const int8_t* win, int8_t* planes, int
         for (int q = 0; q < 4; ++q) w[q] = __builtin_amdgcn_alignbyte(e[q + 1], e[q], 2);
       }
       uint4 iu, qu;
-      splitWords(w, iu, qu);
+      int8IqToF16Units(w, iu, qu);
       const int unit = planeUnit(g >> 2, g & 3);
       *reinterpret_cast<uint4*>(planes + 16 * unit) = iu;
       *reinterpret_cast<uint4*>(planes + G::kPlaneBytes + 16 * unit) = qu;

@@ -41,6 +41,12 @@ bool firCfMfmaEligible(size_t tapCount, size_t decimation, const void* in);
 hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, size_t decimation, void* out,
                            size_t nOut, int epi, hipStream_t stream);
 
+// int8 IQ input (2-byte aligned) x real taps, D <= 16, 31 D + T <= 1408, T >= 5 D, on f16 MFMA
+// (fir_cf_mfma.hip).
+bool firI8DecMfmaEligible(size_t tapCount, size_t decimation, const void* in);
+hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCount, size_t decimation, void* out,
+                              size_t nOut, int epi, hipStream_t stream);
+
 // Kernel-selection policy bits (gsdrAmdSetKernelPolicy).
 uint32_t kernelPolicy();
 

@@ -32,4 +32,30 @@ __device__ __forceinline__ uint32_t xcdTile(uint32_t b, uint32_t nb) {
 
 __device__ __forceinline__ int waveUniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+// Four interleaved int8 IQ words (I0 Q0 I1 Q1 each) -> the clamped samples x' = max(x, -127) of
+// gsdrInt8ToNormFloat's numerator as f16 I and Q units (8 samples each), exactly.
+// u = x ^ 0x80 = x + 128 lands in the low byte of the f16 1024 + u (high byte 0x64); adding
+// -1152 gives x exactly, and max(., -127) is the reference's fmaxf(-1, x/127) clamp.
+__device__ __forceinline__ void int8IqToF16Units(const uint32_t (&w)[4], uint4& iu, uint4& qu) {
+  const h2 bias = {(_Float16)-1152.0f, (_Float16)-1152.0f};
+  const h2 lo = {(_Float16)-127.0f, (_Float16)-127.0f};
+  uint32_t ri[4], rq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t u = w[q] ^ 0x80808080u;
+    const uint32_t pi = __builtin_amdgcn_perm(0x64646464u, u, 0x04020400u);
+    const uint32_t pq = __builtin_amdgcn_perm(0x64646464u, u, 0x04030401u);
+    h2 fi = __builtin_bit_cast(h2, pi) + bias;
+    h2 fq = __builtin_bit_cast(h2, pq) + bias;
+    fi = __builtin_elementwise_max(fi, lo);
+    fq = __builtin_elementwise_max(fq, lo);
+    ri[q] = __builtin_bit_cast(uint32_t, fi);
+    rq[q] = __builtin_bit_cast(uint32_t, fq);
+  }
+  iu = uint4{ri[0], ri[1], ri[2], ri[3]};
+  qu = uint4{rq[0], rq[1], rq[2], rq[3]};
+}
+
 }  // namespace gsdr_amd

@@ -1,0 +1,351 @@
+// AM receive chain executor (include/gsdr/gsdr_amd.h, gsdrAmChain*): the C5 chain
+// int8 IQ -> cf32 -> FC FIR -> AM -> FF FIR as one hipGraph per step.
+//
+// Stream semantics are those of the reference filters stepped one chunk at a time
+// (Fir::getNumOutputElements / readOutput, Fir.cpp:141-279; QuadAmDemod.cpp:80-107;
+// Int8ToFloat.cpp:80-100): the first chunk yields floor((L - T + 1) / D) RF outputs, after which
+// every chunk of L samples yields exactly L / D, and the FIR keeps
+//     r = T - 1 + ((L - T + 1) mod D)
+// input samples between steps (Appendix A of SURVEY.md: same count rule, no wrap). The audio FIR
+// behaves the same way on the AM stream (ra retained). With fixed r and ra every buffer of the
+// steady state sits at a fixed address, so the step is captured once:
+//
+//   staging[p] = [ r history | L new ]  int8 IQ     (p = step parity; the carry goes to 1 - p)
+//   am         = [ ra history | L/D new ] f32
+//   graph(p):  gsdrInt8FirFCAmDemod(staging[p] -> am + ra)        (L/D outputs)
+//              copy staging[p][L, L + r) -> staging[1-p][0, r)     (RF history)
+//              gsdrFirFF(am -> audio)                              (L/(D Da) outputs)
+//              copy am[La, La + ra) -> am[0, ra)                   (audio history)
+//
+// The first step has its own graph (input at staging[0] + r, AM written to the end of the window).
+// Resident streams (gsdrAmChainStepResident) skip the staging window: the RF history is read in
+// place in front of the caller's chunks and the whole multi-chunk segment is three launches.
+// The chunk copy into staging[p] + r happens outside the graph (its source changes per step); in
+// the pinned-ring mode it runs on a second stream, ordered by events against the step that last
+// read staging[p], so it overlaps the previous step's compute.
+#include <gsdr/gsdr_amd.h>
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+#include <vector>
+
+namespace {
+
+#define AMC_TRY(expr__)                      \
+  do {                                       \
+    const hipError_t e__ = (expr__);         \
+    if (e__ != hipSuccess) return e__;       \
+  } while (false)
+
+size_t firCount(size_t n, size_t T, size_t D) { return n < T ? 0 : (n - (T - 1)) / D; }  // Fir.cpp:178-186
+
+}  // namespace
+
+struct gsdrAmChainImpl {
+  int32_t device = 0;
+  size_t T = 0, D = 1, Ta = 0, Da = 1, L = 0, La = 0;
+  size_t r = 0, ra = 0;    // retained input / AM samples between steps
+  size_t n1 = 0, na1 = 0;  // first-step RF / audio output counts
+  size_t naSteady = 0;
+  float* taps = nullptr;
+  float* audioTaps = nullptr;
+  int8_t* staging[2] = {nullptr, nullptr};
+  float* am = nullptr;
+  float* audio = nullptr;
+  hipStream_t stream = nullptr;
+  hipStream_t copyStream = nullptr;
+  hipGraphExec_t first = nullptr;
+  hipGraphExec_t steady[2] = {nullptr, nullptr};
+  hipEvent_t readDone[2] = {nullptr, nullptr};  // staging[p] no longer read by the step that used it
+  hipEvent_t copyDone[2] = {nullptr, nullptr};
+  size_t steps = 0;
+  // resident mode: [ra history | nChunks * La] AM window and its cached graph
+  float* amBig = nullptr;
+  size_t amBigChunks = 0;
+  hipGraphExec_t resident = nullptr;
+  const int8_t* resIn = nullptr;
+  float* resOut = nullptr;
+  size_t resChunks = 0;
+  bool resFirst = false;
+  // pinned ring
+  size_t slots = 0;
+  int8_t* hostIn = nullptr;
+  float* hostOut = nullptr;
+  std::vector<hipEvent_t> slotDone;
+
+  size_t nextOutputs() const { return steps == 0 ? na1 : naSteady; }
+
+  hipError_t capture(hipGraphExec_t* exec, bool firstStep, int p) {
+    hipGraph_t g = nullptr;
+    AMC_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    hipError_t e = enqueueCompute(firstStep, p);
+    hipError_t e2 = hipStreamEndCapture(stream, &g);
+    if (e == hipSuccess) e = e2;
+    if (e == hipSuccess) e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+    if (g != nullptr) (void)hipGraphDestroy(g);
+    return e;
+  }
+
+  hipError_t enqueueCompute(bool firstStep, int p) {
+    const size_t amStart = firstStep ? ra + La - n1 : 0;  // first step: AM at the end of the window
+    const int8_t* in = firstStep ? staging[p] + 2 * r : staging[p];
+    const size_t nRf = firstStep ? n1 : La;
+    AMC_TRY(gsdrInt8FirFCAmDemod(D, taps, T, in, am + (firstStep ? amStart : ra), nRf, device, stream));
+    AMC_TRY(hipMemcpyAsync(staging[1 - p], staging[p] + 2 * L, 2 * r, hipMemcpyDeviceToDevice, stream));
+    AMC_TRY(gsdrFirFF(Da, audioTaps, Ta, am + amStart, audio, firstStep ? na1 : naSteady, device, stream));
+    AMC_TRY(hipMemcpyAsync(am, am + La, sizeof(float) * ra, hipMemcpyDeviceToDevice, stream));
+    return hipSuccess;
+  }
+
+  hipGraphExec_t graphFor(int p) const { return steps == 0 ? first : steady[p]; }
+
+  // RF outputs / audio outputs of a resident step of nChunks chunks
+  size_t residentRf(size_t nChunks) const { return steps == 0 ? firCount(nChunks * L, T, D) : nChunks * La; }
+  size_t residentAudio(size_t nChunks) const {
+    const size_t nRf = residentRf(nChunks);
+    return steps == 0 ? firCount(nRf, Ta, Da) : nChunks * naSteady;
+  }
+
+  hipError_t enqueueResident(const int8_t* in, size_t nChunks, float* out) {
+    const size_t nRf = residentRf(nChunks);
+    const size_t end = ra + nChunks * La;  // the AM window ends here in both cases
+    const size_t amStart = steps == 0 ? end - nRf : 0;
+    const int8_t* rfIn = steps == 0 ? in : in - 2 * r;
+    AMC_TRY(gsdrInt8FirFCAmDemod(D, taps, T, rfIn, amBig + (end - nRf), nRf, device, stream));
+    AMC_TRY(gsdrFirFF(Da, audioTaps, Ta, amBig + amStart, out, residentAudio(nChunks), device, stream));
+    AMC_TRY(hipMemcpyAsync(amBig, amBig + end - ra, sizeof(float) * ra, hipMemcpyDeviceToDevice, stream));
+    return hipSuccess;
+  }
+
+  void release() {
+    if (stream != nullptr) (void)hipStreamSynchronize(stream);
+    if (copyStream != nullptr) (void)hipStreamSynchronize(copyStream);
+    if (first) (void)hipGraphExecDestroy(first);
+    for (auto& g : steady)
+      if (g) (void)hipGraphExecDestroy(g);
+    for (auto& ev : readDone)
+      if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : copyDone)
+      if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : slotDone)
+      if (ev) (void)hipEventDestroy(ev);
+    (void)hipFree(taps);
+    (void)hipFree(audioTaps);
+    (void)hipFree(staging[0]);
+    (void)hipFree(staging[1]);
+    (void)hipFree(am);
+    (void)hipFree(amBig);
+    if (resident) (void)hipGraphExecDestroy(resident);
+    (void)hipFree(audio);
+    if (hostIn) (void)hipHostFree(hostIn);
+    if (hostOut) (void)hipHostFree(hostOut);
+    if (stream) (void)hipStreamDestroy(stream);
+    if (copyStream) (void)hipStreamDestroy(copyStream);
+  }
+};
+
+namespace {
+
+struct DevicePush {  // the reference's CudaDevicePushPop (util/CudaDevicePushPop.h:27-79)
+  int prev = -1;
+  hipError_t err;
+  explicit DevicePush(int dev) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+  }
+  ~DevicePush() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+hipError_t build(gsdrAmChainImpl* c, const gsdrAmChainConfig& cfg) {
+  AMC_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  AMC_TRY(hipStreamCreateWithFlags(&c->copyStream, hipStreamNonBlocking));
+  AMC_TRY(hipMalloc(&c->taps, sizeof(float) * c->T));
+  AMC_TRY(hipMalloc(&c->audioTaps, sizeof(float) * c->Ta));
+  AMC_TRY(hipMemcpy(c->taps, cfg.rfTaps, sizeof(float) * c->T, hipMemcpyHostToDevice));
+  AMC_TRY(hipMemcpy(c->audioTaps, cfg.audioTaps, sizeof(float) * c->Ta, hipMemcpyHostToDevice));
+  for (auto& s : c->staging) AMC_TRY(hipMalloc(&s, 2 * (c->r + c->L)));
+  AMC_TRY(hipMalloc(&c->am, sizeof(float) * (c->ra + c->La)));
+  AMC_TRY(hipMalloc(&c->audio, sizeof(float) * (c->na1 > c->naSteady ? c->na1 : c->naSteady)));
+  for (auto& ev : c->readDone) AMC_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  for (auto& ev : c->copyDone) AMC_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  if (c->slots > 0) {
+    AMC_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hostIn), 2 * c->L * c->slots, hipHostMallocDefault));
+    AMC_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hostOut), sizeof(float) * c->naSteady * c->slots,
+                          hipHostMallocDefault));
+    c->slotDone.assign(c->slots, nullptr);
+    for (auto& ev : c->slotDone) AMC_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+  AMC_TRY(c->capture(&c->first, true, 0));
+  AMC_TRY(c->capture(&c->steady[0], false, 0));
+  AMC_TRY(c->capture(&c->steady[1], false, 1));
+  return hipStreamSynchronize(c->stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t gsdrAmChainCreate(const gsdrAmChainConfig* cfg, int32_t device, gsdrAmChain* chainOut) {
+  if (chainOut == nullptr) return hipErrorInvalidValue;
+  *chainOut = nullptr;
+  if (cfg == nullptr || cfg->rfTaps == nullptr || cfg->audioTaps == nullptr || cfg->rfTapCount == 0 ||
+      cfg->audioTapCount == 0)
+    return hipErrorInvalidValue;
+  gsdrAmChainImpl* c = new (std::nothrow) gsdrAmChainImpl();
+  if (c == nullptr) return hipErrorOutOfMemory;
+  c->device = device;
+  c->T = cfg->rfTapCount;
+  c->D = cfg->rfDecimation < 1 ? 1 : cfg->rfDecimation;
+  c->Ta = cfg->audioTapCount;
+  c->Da = cfg->audioDecimation < 1 ? 1 : cfg->audioDecimation;
+  c->L = cfg->chunkSamples;
+  c->slots = cfg->hostSlots;
+  const bool shapeOk = c->L >= c->T && c->L % (c->D * c->Da) == 0;
+  if (shapeOk) {
+    c->La = c->L / c->D;
+    c->n1 = firCount(c->L, c->T, c->D);
+    c->r = c->L - c->n1 * c->D;  // = T - 1 + ((L - T + 1) mod D)
+    c->na1 = firCount(c->n1, c->Ta, c->Da);
+    c->ra = c->n1 - c->na1 * c->Da;
+    c->naSteady = c->La / c->Da;
+  }
+  // steady state: L/D RF and L/(D Da) audio outputs per step, disjoint history copies
+  if (!shapeOk || c->na1 == 0 || c->r > c->L || c->ra > c->La ||
+      firCount(c->r + c->L, c->T, c->D) != c->La || firCount(c->ra + c->La, c->Ta, c->Da) != c->naSteady) {
+    delete c;
+    return hipErrorInvalidValue;
+  }
+  DevicePush push(device);
+  hipError_t e = push.err;
+  if (e == hipSuccess) e = build(c, *cfg);
+  if (e != hipSuccess) {
+    c->release();
+    delete c;
+    return e;
+  }
+  *chainOut = c;
+  return hipSuccess;
+}
+
+void gsdrAmChainDestroy(gsdrAmChain c) {
+  if (c == nullptr) return;
+  DevicePush push(c->device);
+  c->release();
+  delete c;
+}
+
+hipStream_t gsdrAmChainStream(gsdrAmChain c) { return c == nullptr ? nullptr : c->stream; }
+
+size_t gsdrAmChainNextOutputCount(gsdrAmChain c) { return c == nullptr ? 0 : c->nextOutputs(); }
+
+hipError_t gsdrAmChainStep(gsdrAmChain c, const int8_t* inputIq, float* output, size_t* outputCount) {
+  if (c == nullptr || inputIq == nullptr || output == nullptr) return hipErrorInvalidValue;
+  DevicePush push(c->device);
+  AMC_TRY(push.err);
+  const int p = c->steps == 0 ? 0 : (int)(c->steps & 1);
+  const size_t n = c->nextOutputs();
+  AMC_TRY(hipMemcpyAsync(c->staging[p] + 2 * c->r, inputIq, 2 * c->L, hipMemcpyDeviceToDevice, c->stream));
+  AMC_TRY(hipGraphLaunch(c->graphFor(p), c->stream));
+  AMC_TRY(hipEventRecord(c->readDone[p], c->stream));
+  AMC_TRY(hipMemcpyAsync(output, c->audio, sizeof(float) * n, hipMemcpyDeviceToDevice, c->stream));
+  ++c->steps;
+  if (outputCount != nullptr) *outputCount = n;
+  return hipSuccess;
+}
+
+int8_t* gsdrAmChainHostInputSlot(gsdrAmChain c, size_t slot) {
+  return c == nullptr || slot >= c->slots ? nullptr : c->hostIn + 2 * c->L * slot;
+}
+
+const float* gsdrAmChainHostOutputSlot(gsdrAmChain c, size_t slot) {
+  return c == nullptr || slot >= c->slots ? nullptr : c->hostOut + c->naSteady * slot;
+}
+
+hipError_t gsdrAmChainStepHost(gsdrAmChain c, size_t slot, size_t* outputCount) {
+  if (c == nullptr || slot >= c->slots) return hipErrorInvalidValue;
+  DevicePush push(c->device);
+  AMC_TRY(push.err);
+  const int p = c->steps == 0 ? 0 : (int)(c->steps & 1);
+  const size_t n = c->nextOutputs();
+  // the H2D copy may start once the step that last read staging[p] is done with it
+  AMC_TRY(hipStreamWaitEvent(c->copyStream, c->readDone[p], 0));
+  AMC_TRY(hipMemcpyAsync(c->staging[p] + 2 * c->r, c->hostIn + 2 * c->L * slot, 2 * c->L, hipMemcpyHostToDevice,
+                         c->copyStream));
+  AMC_TRY(hipEventRecord(c->copyDone[p], c->copyStream));
+  AMC_TRY(hipStreamWaitEvent(c->stream, c->copyDone[p], 0));
+  AMC_TRY(hipGraphLaunch(c->graphFor(p), c->stream));
+  AMC_TRY(hipEventRecord(c->readDone[p], c->stream));
+  AMC_TRY(hipMemcpyAsync(c->hostOut + c->naSteady * slot, c->audio, sizeof(float) * n, hipMemcpyDeviceToHost,
+                         c->stream));
+  AMC_TRY(hipEventRecord(c->slotDone[slot], c->stream));
+  ++c->steps;
+  if (outputCount != nullptr) *outputCount = n;
+  return hipSuccess;
+}
+
+hipError_t gsdrAmChainWaitSlot(gsdrAmChain c, size_t slot) {
+  if (c == nullptr || slot >= c->slots) return hipErrorInvalidValue;
+  return hipEventSynchronize(c->slotDone[slot]);
+}
+
+size_t gsdrAmChainResidentOutputCount(gsdrAmChain c, size_t nChunks) {
+  return c == nullptr ? 0 : c->residentAudio(nChunks);
+}
+
+hipError_t gsdrAmChainStepResident(gsdrAmChain c, const int8_t* inputIq, size_t nChunks, float* output,
+                                   size_t* outputCount) {
+  if (c == nullptr || inputIq == nullptr || output == nullptr || nChunks == 0) return hipErrorInvalidValue;
+  DevicePush push(c->device);
+  AMC_TRY(push.err);
+  if (nChunks > c->amBigChunks) {  // grow the AM window (outside any capture)
+    AMC_TRY(hipStreamSynchronize(c->stream));
+    (void)hipFree(c->amBig);
+    c->amBig = nullptr;
+    c->amBigChunks = 0;
+    AMC_TRY(hipMalloc(&c->amBig, sizeof(float) * (c->ra + nChunks * c->La)));
+    c->amBigChunks = nChunks;
+    if (c->resident) (void)hipGraphExecDestroy(c->resident);
+    c->resident = nullptr;
+  }
+  const bool firstStep = c->steps == 0;
+  if (c->resident == nullptr || c->resIn != inputIq || c->resOut != output || c->resChunks != nChunks ||
+      c->resFirst != firstStep) {
+    if (c->resident) (void)hipGraphExecDestroy(c->resident);
+    c->resident = nullptr;
+    hipGraph_t g = nullptr;
+    AMC_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    hipError_t e = c->enqueueResident(inputIq, nChunks, output);
+    const hipError_t e2 = hipStreamEndCapture(c->stream, &g);
+    if (e == hipSuccess) e = e2;
+    if (e == hipSuccess) e = hipGraphInstantiate(&c->resident, g, nullptr, nullptr, 0);
+    if (g != nullptr) (void)hipGraphDestroy(g);
+    AMC_TRY(e);
+    c->resIn = inputIq;
+    c->resOut = output;
+    c->resChunks = nChunks;
+    c->resFirst = firstStep;
+  }
+  const size_t n = c->residentAudio(nChunks);
+  AMC_TRY(hipGraphLaunch(c->resident, c->stream));
+  // the AM history now sits at the front of amBig; the per-chunk window `am` is stale, so a later
+  // per-chunk step would need a reset (documented in gsdr_amd.h)
+  c->steps += nChunks;
+  if (outputCount != nullptr) *outputCount = n;
+  return hipSuccess;
+}
+
+hipError_t gsdrAmChainReset(gsdrAmChain c) {
+  if (c == nullptr) return hipErrorInvalidValue;
+  DevicePush push(c->device);
+  AMC_TRY(push.err);
+  AMC_TRY(hipStreamSynchronize(c->copyStream));
+  AMC_TRY(hipStreamSynchronize(c->stream));
+  c->steps = 0;
+  return hipSuccess;
+}
+
+}  // extern "C"

@@ -76,6 +76,65 @@ GSDR_API hipError_t gsdrSynthWidebandCf32(uint64_t seed, double f1, double f2Cyc
                                           hipFloatComplex* output, size_t numSamples, int32_t device,
                                           hipStream_t stream);
 
+/*
+ * AM receive chain executor (C5: int8 IQ -> cf32 -> FC FIR (rf taps, rf decimation) -> AM ->
+ * FF FIR (audio taps, audio decimation)), stepping fixed chunks of `chunkSamples` IQ samples.
+ *
+ * Output is exactly what the reference filters chained by a SteppingDriver produce from the same
+ * stream (Fir count rule Fir.cpp:178-186 at both FIRs; the first step emits fewer samples), but
+ * the steady-state step is ONE hipGraph launch (FIR+AM kernel, history carries, audio FIR) captured
+ * at creation, with every buffer at a fixed address: a [history | chunk] staging window per parity
+ * (double-buffered so the next chunk's copy overlaps the current step) and an
+ * [audio history | AM] window.
+ *
+ * chunkSamples must be a multiple of rfDecimation * audioDecimation and at least
+ * rfTapCount + audioTapCount * rfDecimation (so the first step yields audio).
+ * Taps are host memory (copied). hostSlots > 0 adds a ring of pinned (hipHostMalloc) input /
+ * output slots for gsdrAmChainStepHost; its H2D copies run on a second stream and overlap the
+ * previous step's compute.
+ */
+typedef struct gsdrAmChainImpl* gsdrAmChain;
+
+typedef struct {
+  const float* rfTaps;
+  size_t rfTapCount;
+  size_t rfDecimation;
+  const float* audioTaps;
+  size_t audioTapCount;
+  size_t audioDecimation;
+  size_t chunkSamples;
+  size_t hostSlots;
+} gsdrAmChainConfig;
+
+GSDR_API hipError_t gsdrAmChainCreate(const gsdrAmChainConfig* config, int32_t device, gsdrAmChain* chainOut);
+GSDR_API void gsdrAmChainDestroy(gsdrAmChain chain);
+/* Stream every step is enqueued on (non-blocking, created with the chain). */
+GSDR_API hipStream_t gsdrAmChainStream(gsdrAmChain chain);
+/* Audio samples the NEXT step will produce. */
+GSDR_API size_t gsdrAmChainNextOutputCount(gsdrAmChain chain);
+/* One step from device memory: chunkSamples IQ pairs at inputIq (copied into the staging window),
+ * audio written to `output` (device, gsdrAmChainNextOutputCount floats). Asynchronous. */
+GSDR_API hipError_t gsdrAmChainStep(gsdrAmChain chain, const int8_t* inputIq, float* output, size_t* outputCount);
+/* Pinned ring. Fill input slot k (chunkSamples IQ pairs), call StepHost(k); after WaitSlot(k) the
+ * output slot k holds *outputCount audio samples. A slot may be refilled after its WaitSlot. */
+GSDR_API int8_t* gsdrAmChainHostInputSlot(gsdrAmChain chain, size_t slot);
+GSDR_API const float* gsdrAmChainHostOutputSlot(gsdrAmChain chain, size_t slot);
+GSDR_API hipError_t gsdrAmChainStepHost(gsdrAmChain chain, size_t slot, size_t* outputCount);
+GSDR_API hipError_t gsdrAmChainWaitSlot(gsdrAmChain chain, size_t slot);
+/* Resident stream: nChunks consecutive chunks at `inputIq` (device), processed as ONE captured
+ * graph of three launches (RF FIR + AM over all nChunks * chunkSamples samples, the audio FIR over
+ * the whole AM segment, the audio history carry), audio written to `output` (device). After the
+ * first step the chain's RF history is read in place: the rfTapCount - 1 (+ < rfDecimation)
+ * samples in front of inputIq must be the stream's preceding samples, as they are in a contiguous
+ * stream buffer. The graph is cached for the last (inputIq, nChunks, output) and replayed. Output
+ * count: gsdrAmChainResidentOutputCount. Do not interleave with gsdrAmChainStep/StepHost on the
+ * same stream position (those keep the RF history in the staging window instead). */
+GSDR_API size_t gsdrAmChainResidentOutputCount(gsdrAmChain chain, size_t nChunks);
+GSDR_API hipError_t gsdrAmChainStepResident(gsdrAmChain chain, const int8_t* inputIq, size_t nChunks, float* output,
+                                            size_t* outputCount);
+/* Forget all history: the next step is a first step again. */
+GSDR_API hipError_t gsdrAmChainReset(gsdrAmChain chain);
+
 #ifdef __cplusplus
 }
 #endif

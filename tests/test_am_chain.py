@@ -1,0 +1,130 @@
+"""The C5 AM receive chain executor (gsdrAmChain*: int8 IQ -> cf32 -> FC FIR -> AM -> FF FIR, one
+hipGraph per step) against the oracle chain over the whole stream: the reference filters stepped
+chunk by chunk give exactly the whole-stream result under the Fir count rule (Fir.cpp:178-186),
+so the concatenated step outputs must equal the float64 chain on the concatenated input."""
+import numpy as np
+import pytest
+
+FIR_TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def chain_mod():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from gpusdr import chain
+    return chain
+
+
+def _expected(orc, iq, rf_taps, D, audio_taps, Da):
+    """float64 chain + per-sample tolerance: the RF FIR bound and the sqrt rounding carried through
+    the audio FIR's |taps|, plus the audio FIR's own bound."""
+    x = orc.int8_to_float(iq).view(np.complex64)
+    y, rf_bound = orc.fir_f64(rf_taps, x, D)
+    am = np.abs(y)
+    audio, audio_bound = orc.fir_f64(audio_taps, am.astype(np.float32), Da)
+    n = len(audio)
+    carried, _ = orc.fir_f64(np.abs(audio_taps), (FIR_TOL * (rf_bound + am)).astype(np.float32), Da, n)
+    return audio, carried + FIR_TOL * audio_bound + 1e-30
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,D,Ta,Da,L", [(1023, 10, 255, 20, 4000), (1023, 10, 255, 20, 40000),
+                                         (127, 1, 63, 4, 2048), (64, 3, 31, 5, 3000)])
+def test_am_chain_device_steps(chain_mod, orc, T, D, Ta, Da, L):
+    import torch
+    rng = np.random.default_rng(T + L)
+    rf = orc.lowpass_taps(T, 0.4 / D)
+    au = orc.lowpass_taps(Ta, 0.4 / Da)
+    c = chain_mod.AmChain(rf, D, au, Da, L)
+    steps = 7
+    iq = rng.integers(-128, 128, size=2 * L * steps).astype(np.int8)
+    dev = torch.from_numpy(iq).cuda()
+    outs = []
+    for s in range(steps):
+        outs.append(c.step(dev[2 * L * s: 2 * L * (s + 1)]).cpu().numpy())
+    got = np.concatenate(outs)
+    want, bound = _expected(orc, iq, rf, D, au, Da)
+    assert len(got) == len(want)
+    # every step after the first yields L / (D Da) samples
+    assert all(len(o) == L // (D * Da) for o in outs[1:])
+    assert np.all(np.abs(got - want) <= bound)
+    c.close()
+
+
+@pytest.mark.gpu
+def test_am_chain_host_ring_matches_device(chain_mod, orc):
+    """Pinned-ring steps (H2D on a second stream, double-buffered staging) give bit-identical
+    output to the device-input steps; reset() starts a fresh stream."""
+    import torch
+    T, D, Ta, Da, L = 255, 5, 63, 8, 8000
+    rng = np.random.default_rng(5)
+    rf = orc.lowpass_taps(T, 0.08)
+    au = orc.lowpass_taps(Ta, 0.05)
+    steps = 9
+    iq = rng.integers(-128, 128, size=2 * L * steps).astype(np.int8)
+    dev_chain = chain_mod.AmChain(rf, D, au, Da, L)
+    dev = torch.from_numpy(iq).cuda()
+    ref = [dev_chain.step(dev[2 * L * s: 2 * L * (s + 1)]).cpu().numpy() for s in range(steps)]
+    host_chain = chain_mod.AmChain(rf, D, au, Da, L, host_slots=3)
+    for attempt in range(2):  # the second pass after reset() must repeat the first exactly
+        pending = []
+        got = []
+        for s in range(steps):
+            slot = s % 3
+            if len(pending) == 3:  # a slot is refilled only after its step finished
+                ps, pn = pending.pop(0)
+                got.append(host_chain.wait_host(ps, pn))
+            host_chain.host_input(slot)[:] = iq[2 * L * s: 2 * L * (s + 1)]
+            pending.append((slot, host_chain.step_host(slot)))
+        for ps, pn in pending:
+            got.append(host_chain.wait_host(ps, pn))
+        assert len(got) == steps
+        for a, b in zip(got, ref):
+            assert a.tobytes() == b.tobytes()
+        host_chain.reset()
+    want, bound = _expected(orc, iq, rf, D, au, Da)
+    assert np.all(np.abs(np.concatenate(ref) - want) <= bound)
+
+
+@pytest.mark.gpu
+def test_am_chain_rejects_bad_shapes(chain_mod, orc):
+    rf = orc.lowpass_taps(127, 0.1)
+    au = orc.lowpass_taps(63, 0.1)
+    for L in (1000 + 1, 100):  # not a multiple of D * Da; too short for one audio sample
+        with pytest.raises(Exception):
+            chain_mod.AmChain(rf, 4, au, 5, L)
+
+
+@pytest.mark.gpu
+def test_am_chain_resident_stream(chain_mod, orc):
+    """Resident mode: whole multi-chunk segments of one contiguous device stream per step (RF
+    history read in place, one cached graph per segment shape) against the chunk-by-chunk steps
+    and the oracle chain."""
+    import torch
+    T, D, Ta, Da, L = 1023, 10, 255, 20, 4000
+    rng = np.random.default_rng(11)
+    rf = orc.lowpass_taps(T, 0.04)
+    au = orc.lowpass_taps(Ta, 0.02)
+    plan = [3, 2, 2, 4, 1]
+    total = sum(plan)
+    iq = rng.integers(-128, 128, size=2 * L * total).astype(np.int8)
+    dev = torch.from_numpy(iq).cuda()
+    res = chain_mod.AmChain(rf, D, au, Da, L)
+    got, pos = [], 0
+    for n in plan:
+        out = torch.empty(res.resident_output_count(n), dtype=torch.float32, device="cuda")
+        cnt = res.step_resident(dev[2 * L * pos:], n, out)
+        got.append(out[:cnt].cpu().numpy())
+        pos += n
+    got = np.concatenate(got)
+    per = chain_mod.AmChain(rf, D, au, Da, L)
+    ref = np.concatenate([per.step(dev[2 * L * s: 2 * L * (s + 1)]).cpu().numpy() for s in range(total)])
+    assert len(got) == len(ref)
+    want, bound = _expected(orc, iq, rf, D, au, Da)
+    # tile boundaries differ between the two modes, so the split-K sums group differently: both
+    # meet the oracle bound, and each other within twice it
+    assert np.all(np.abs(got - want) <= bound)
+    assert np.all(np.abs(ref - want) <= bound)
+    assert np.all(np.abs(got - ref) <= 2 * bound)

@@ -224,6 +224,50 @@ def test_int8_mfma_misaligned_falls_back(ops, orc):
         _check_fir(y, y64, bound, ("misaligned", off))
 
 
+I8_DEC_CASES = [(1023, 10, 20000), (1023, 10, 1), (255, 5, 3001), (64, 3, 777), (300, 1, 5000),
+                (1346, 2, 2049), (127, 16, 4096), (1023, 2, 777)]
+
+
+@pytest.mark.parametrize("T,D,n_out", I8_DEC_CASES)
+def test_int8_decimating_mfma_path(ops, orc, T, D, n_out):
+    """int8 IQ x real taps on the split-K Toeplitz f16 MFMA kernel (D > 1 or T > 129; the C5 RF
+    stage): against the float64 oracle, AM within a few ulp of AM of the complex output, and
+    against the fp32 VALU kernel."""
+    rng = np.random.default_rng(T * 13 + D)
+    n_in = (n_out - 1) * D + T
+    iq = rng.integers(-128, 128, size=2 * n_in).astype(np.int8)
+    iq[:64] = -128
+    taps = orc.lowpass_taps(T, 0.4 / D).astype(np.float32)
+    taps[T // 3] *= -2.0
+    iq_d, taps_d = _dev(iq), _dev(taps)
+    y = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))
+    am = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=True))
+    x = orc.int8_to_float(iq).view(np.complex64)
+    y64, bound = orc.fir_f64(taps, x, D, n_out)
+    _check_fir(y, y64, bound, ("i8-dec-mfma", T, D, n_out))
+    am_ref = orc.quad_am_demod(y)
+    assert np.all(np.abs(am - am_ref) <= 4 * np.spacing(am_ref))
+    assert np.all(np.abs(am - np.abs(y64)) <= FIR_TOL * bound + 1e-30)
+    prev = ops.set_kernel_policy(ops.POLICY_NO_MFMA)
+    try:
+        y_valu = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))
+    finally:
+        ops.set_kernel_policy(prev)
+    assert np.all(np.abs(y.astype(np.complex128) - y_valu) <= 2 * FIR_TOL * bound + 1e-30)
+
+
+def test_int8_decimating_mfma_misaligned(ops, orc):
+    """Any sample-aligned input takes the MFMA kernel (dword loads + byte funnel shift)."""
+    rng = np.random.default_rng(78)
+    T, D, n_out = 1023, 10, 3000
+    iq = rng.integers(-128, 128, size=2 * ((n_out - 1) * D + T) + 16).astype(np.int8)
+    taps = orc.lowpass_taps(T, 0.04)
+    for off in (2, 4, 6, 14):
+        y = _host(ops.fir(_dev(taps), _dev(iq)[off:], D, n_out, int8_iq=True))
+        y64, bound = orc.fir_f64(taps, orc.int8_to_float(iq[off:]).view(np.complex64), D, n_out)
+        _check_fir(y, y64, bound, ("i8-dec-misaligned", off))
+
+
 CF_MFMA_CASES = [(64, 1, 1000), (127, 3, 5000), (255, 2, 777), (1023, 10, 20000), (1023, 1, 4113),
                  (600, 16, 3000), (1023, 5, 1), (300, 7, 2049)]
 
