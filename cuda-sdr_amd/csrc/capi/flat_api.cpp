@@ -109,6 +109,10 @@ uint32_t gspNamedQueueCreate(const char* queueId, const char* json) {
   return factories()->getCommandQueueFactory()->create(queueId, json);
 }
 
+uint32_t gspNamedQueueGet(const char* queueId, gspHandle* queueOut) {
+  return give(factories()->getCommandQueueFactory()->getCudaCommandQueue(queueId), queueOut);
+}
+
 uint32_t gspNodeCreate(const char* name, const char* json, gspHandle* nodeOut) {
   if (!hasNodeFactory("Fir")) {
     const Status st = registerDefaultNodeFactories();

@@ -103,6 +103,28 @@ __global__ __launch_bounds__(kBlock) void cosineC(float phi0, float step, f2* __
   }
 }
 
+// ---- complex multiply / FM discriminator --------------------------------------------------------------
+__device__ __forceinline__ f2 cmul(f2 a, f2 b) {
+  return f2{fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x)};
+}
+
+__global__ __launch_bounds__(kBlock) void multiplyCC(const f2* __restrict__ a, const f2* __restrict__ b,
+                                                     f2* __restrict__ out, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock)
+    out[i] = cmul(a[i], b[i]);
+}
+
+// each thread reads its sample and the next one (the neighbour's read hits L1/L2)
+__global__ __launch_bounds__(kBlock) void quadFmDemod(const f2* __restrict__ in, float* __restrict__ out, float gain,
+                                                      size_t n) {
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) {
+    const f2 z0 = in[i], z1 = in[i + 1];
+    const float re = fmaf(z1.x, z0.x, z1.y * z0.y);
+    const float im = fmaf(z1.y, z0.x, -(z1.x * z0.y));
+    out[i] = gain * atan2f(im, re);
+  }
+}
+
 // ---- synthetic sources ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -232,6 +254,29 @@ hipError_t gsdrCosineC(float phiBegin, float phiEnd, hipFloatComplex* output, si
   const float step = (phiEnd - phiBegin) / (float)numElements;
   hipLaunchKernelGGL(cosineC, dim3(blocksFor(numElements)), dim3(kBlock), 0, stream, phiBegin, step,
                      reinterpret_cast<f2*>(output), numElements);
+  return hipGetLastError();
+}
+
+hipError_t gsdrMultiplyCC(const hipFloatComplex* a, const hipFloatComplex* b, hipFloatComplex* output,
+                          size_t numElements, int32_t device, hipStream_t stream) {
+  if (numElements == 0) return hipSuccess;
+  if (a == nullptr || b == nullptr || output == nullptr) return hipErrorInvalidValue;
+  DevicePush push(device);
+  if (!push.ok) return hipErrorInvalidDevice;
+  hipLaunchKernelGGL(multiplyCC, dim3(blocksFor(numElements)), dim3(kBlock), 0, stream,
+                     reinterpret_cast<const f2*>(a), reinterpret_cast<const f2*>(b), reinterpret_cast<f2*>(output),
+                     numElements);
+  return hipGetLastError();
+}
+
+hipError_t gsdrQuadFmDemod(const hipFloatComplex* input, float* output, float gain, size_t numOutputs, int32_t device,
+                           hipStream_t stream) {
+  if (numOutputs == 0) return hipSuccess;
+  if (input == nullptr || output == nullptr) return hipErrorInvalidValue;
+  DevicePush push(device);
+  if (!push.ok) return hipErrorInvalidDevice;
+  hipLaunchKernelGGL(quadFmDemod, dim3(blocksFor(numOutputs)), dim3(kBlock), 0, stream,
+                     reinterpret_cast<const f2*>(input), output, gain, numOutputs);
   return hipGetLastError();
 }
 

@@ -29,6 +29,8 @@
 #include <gsdr/gsdr_amd.h>
 
 #include <atomic>
+#include <cmath>
+#include <type_traits>
 
 namespace gsdr_amd {
 
@@ -54,7 +56,21 @@ struct FirArgs {
   int32_t gtot;        // total 8-tap groups over all phases
   int32_t regionRows;  // LDS rows per phase region
   int32_t tileOutputs; // outputs per tile (per stream for FF)
+  int32_t mix;         // complex input only: multiply sample n by exp(j theta(n)) first
+  uint64_t mixPhase0;  // theta(n) = 2 pi (mixPhase0 + n mixStep) / 2^64: cycle fractions, so the
+  uint64_t mixStep;    // phase wraps exactly (mod 2 pi) at any stream position
 };
+
+// Frequency shifter fused into the sample load (ComplexCosineSource x MultiplyCcc in
+// front of the FIR): z * exp(j theta(n)) with theta reduced exactly in 64-bit fixed point, then
+// evaluated in float; the product uses the gsdrMultiplyCC expression.
+__device__ __forceinline__ f2 mixSample(const FirArgs& a, int64_t n, f2 z) {
+  const uint64_t ph = a.mixPhase0 + (uint64_t)n * a.mixStep;
+  const float th = (float)((double)(int64_t)ph * 3.4061215800865545e-19);  // 2 pi / 2^64
+  float sn, cs;
+  sincosf(th, &sn, &cs);
+  return f2{fmaf(z.x, cs, -(z.y * sn)), fmaf(z.x, sn, z.y * cs)};
+}
 
 template <int MODE, int INK>
 __device__ __forceinline__ f2 loadElement(const FirArgs& a, int64_t gi) {
@@ -75,6 +91,9 @@ __device__ __forceinline__ f2 loadElement(const FirArgs& a, int64_t gi) {
     } else {  // CF: broadcast the real sample to both lanes of the pair
       if (gi < a.nIn) z.x = z.y = x[gi];
     }
+  }
+  if constexpr (INK == kInCF32 || INK == kInI8IQ) {
+    if (a.mix) z = mixSample(a, gi, z);  // kernel-uniform branch
   }
   return z;
 }
@@ -327,6 +346,9 @@ __global__ __launch_bounds__(kThreads) void firDirectKernel(FirArgs a) {
       const float x = reinterpret_cast<const float*>(a.in)[base + j];
       z = f2{x, x};
     }
+    if constexpr (INK == kInCF32 || INK == kInI8IQ) {
+      if (a.mix) z = mixSample(a, base + j, z);
+    }
     if (MODE == kFirFF || MODE == kFirFC) {
       acc = __builtin_elementwise_fma(f2{a.taps[j], a.taps[j]}, z, acc);
     } else if (MODE == kFirCF) {
@@ -372,9 +394,10 @@ struct SmallElem<kInI8IQ> {
 // writes over the banks)
 __host__ __device__ inline int smallRows(int T, int D) { return (kThreads + (T + D - 1) / D) | 1; }
 
-template <int MODE, int INK, int EPI>
+template <int MODE, int INK, int EPI, bool MIX = false>
 __global__ __launch_bounds__(kThreads) void firSmallKernel(FirArgs a) {
-  typedef typename SmallElem<INK>::T E;
+  // mixing stages the rotated samples as cf32
+  typedef typename std::conditional<MIX, f2, typename SmallElem<INK>::T>::type E;
   constexpr int kTapF = (MODE == kFirCC || MODE == kFirCF) ? 2 : 1;  // floats per tap
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int D = a.D, T = a.T;
@@ -388,7 +411,7 @@ __global__ __launch_bounds__(kThreads) void firSmallKernel(FirArgs a) {
   const int64_t avail = a.nIn - base;
   const int64_t span = (int64_t)(kThreads - 1) * D + T;
   const int nWin = (int)(avail < span ? avail : span);
-  const E* src = reinterpret_cast<const E*>(a.in) + base;
+  const E* src = reinterpret_cast<const E*>(a.in) + base;  // (unused when MIX)
   // staging: 8 independent loads in flight per thread before the scattered LDS stores (a plain
   // loop waits out the HBM latency once per element); i / D through a float reciprocal, corrected
   const float invD = 1.0f / (float)D;
@@ -397,7 +420,19 @@ __global__ __launch_bounds__(kThreads) void firSmallKernel(FirArgs a) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + u * kThreads + (int)threadIdx.x;
-      v[u] = src[i < nWin ? i : nWin - 1];
+      const int ic = i < nWin ? i : nWin - 1;
+      if constexpr (MIX) {
+        f2 z;
+        if constexpr (INK == kInI8IQ) {
+          const char2 c = reinterpret_cast<const char2*>(a.in)[base + ic];
+          z = f2{int8ToNorm(c.x), int8ToNorm(c.y)};
+        } else {
+          z = reinterpret_cast<const f2*>(a.in)[base + ic];
+        }
+        v[u] = mixSample(a, base + ic, z);
+      } else {
+        v[u] = src[ic];
+      }
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -429,7 +464,7 @@ __global__ __launch_bounds__(kThreads) void firSmallKernel(FirArgs a) {
 #pragma unroll 8
       for (int q = qb; q < qe; ++q) {
         f2 z;
-        if constexpr (INK == kInCF32) {
+        if constexpr (INK == kInCF32 || MIX) {
           z = x[q];
         } else if constexpr (INK == kInI8IQ) {
           const char2 v = x[q];
@@ -532,17 +567,23 @@ FirPlanShape planFirShape(size_t tapCount, size_t decimation) {
   return s;
 }
 
+struct MixSpec {
+  bool on = false;
+  uint64_t phase0 = 0, step = 0;
+};
+
 template <int MODE, int INK, int EPI>
 hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t decimation, void* out,
-                     size_t nOut, int32_t device, hipStream_t stream) {
+                     size_t nOut, int32_t device, hipStream_t stream, MixSpec mix = MixSpec{}) {
   if (nOut == 0) return hipSuccess;
   if (in == nullptr || taps == nullptr || out == nullptr || tapCount == 0) return hipErrorInvalidValue;
   if (tapCount > 0x7fffffff || decimation > 0x7fffffff) return hipErrorInvalidValue;
   DevicePush push(device);
   if (!push.ok) return hipErrorInvalidDevice;
 
-  // int8 IQ with real taps: the exact int8 MFMA kernel when the shape allows it
-  if constexpr (MODE == kFirFC && INK == kInI8IQ && EPI != kEpiPair) {
+  // int8 IQ with real taps: the exact int8 MFMA kernel when the shape allows it (the matrix-core
+  // kernels take unmixed samples: a mixed stream is no longer integer)
+  if constexpr (MODE == kFirFC && INK == kInI8IQ && EPI != kEpiPair) if (!mix.on) {
     if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firI8MfmaEligible(tapCount, decimation, in))
       return launchFirI8Mfma(static_cast<const int8_t*>(in), taps, tapCount, out, nOut, EPI, stream);
     // decimating / long filters: the split-K Toeplitz kernel on f16 planes
@@ -550,7 +591,7 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
       return launchFirI8DecMfma(static_cast<const int8_t*>(in), taps, tapCount, decimation, out, nOut, EPI, stream);
   }
   // cf32 with real taps: the split-precision bf16 MFMA kernel for the long-filter shapes
-  if constexpr (MODE == kFirFC && INK == kInCF32 && EPI != kEpiPair) {
+  if constexpr (MODE == kFirFC && INK == kInCF32 && EPI != kEpiPair) if (!mix.on) {
     if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firCfMfmaEligible(tapCount, decimation, in))
       return launchFirCfMfma(static_cast<const float*>(in), taps, tapCount, decimation, out, nOut, EPI, stream);
   }
@@ -566,6 +607,9 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
   a.D = (int32_t)s.decimation;
   a.deff = (int32_t)s.deff;
   a.gtot = (int32_t)s.gtot;
+  a.mix = mix.on ? 1 : 0;
+  a.mixPhase0 = mix.phase0;
+  a.mixStep = mix.step;
 
   if (s.waveOutputSlices == 0) {
     a.tileOutputs = kThreads;
@@ -577,7 +621,7 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
   {
     const int64_t perTile = (int64_t)s.tileOutputs * (MODE == kFirFF ? 2 : 1);
     const int64_t tiles = ((int64_t)nOut + perTile - 1) / perTile;
-    const size_t elem = INK == kInF32 ? 4 : (INK == kInCF32 ? 8 : 2);
+    const size_t elem = INK == kInF32 ? 4 : ((INK == kInCF32 || mix.on) ? 8 : 2);
     const size_t deff = s.decimation < tapCount ? s.decimation : tapCount;
     const size_t qmax = (tapCount + s.decimation - 1) / s.decimation;
     const size_t tapBytes = ((MODE == kFirCC || MODE == kFirCF) ? 8 : 4) * deff * qmax;
@@ -586,10 +630,19 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
     // costs more than the taps; one output per thread over a shared window is faster
     const bool manyPhasesFF = MODE == kFirFF && s.decimation >= 8;
     if ((tiles < 128 || manyPhasesFF) && lds <= kLdsSoftLimit) {
+      const int64_t blocks = ((int64_t)nOut + kThreads - 1) / kThreads;
+      if constexpr (INK == kInCF32 || INK == kInI8IQ) {
+        if (mix.on) {
+          auto kernel = firSmallKernel<MODE, INK, EPI, true>;
+          hipError_t e = ensureLds(kernel, lds);
+          if (e != hipSuccess) return e;
+          hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kThreads), lds, stream, a);
+          return hipGetLastError();
+        }
+      }
       auto kernel = firSmallKernel<MODE, INK, EPI>;
       hipError_t e = ensureLds(kernel, lds);
       if (e != hipSuccess) return e;
-      const int64_t blocks = ((int64_t)nOut + kThreads - 1) / kThreads;
       hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kThreads), lds, stream, a);
       return hipGetLastError();
     }
@@ -614,6 +667,23 @@ uint32_t kernelPolicy() { return gKernelPolicy.load(std::memory_order_relaxed); 
 }  // namespace gsdr_amd
 
 using namespace gsdr_amd;
+
+namespace {
+gsdr_amd::MixSpec mixSpec(double phase0, double radiansPerSample) {
+  // radians -> 64-bit cycle fractions (exact modular phase at any sample index); c in [0, 1), so
+  // c * 2^64 <= 2^64 - 2^11 converts to uint64 without overflow
+  auto toFrac = [](double rad) -> uint64_t {
+    double c = rad / 6.283185307179586476925286766559;
+    c -= std::floor(c);
+    return (uint64_t)std::ldexp(c, 64);
+  };
+  gsdr_amd::MixSpec m;
+  m.on = true;
+  m.phase0 = toFrac(phase0);
+  m.step = toFrac(radiansPerSample);
+  return m;
+}
+}  // namespace
 
 extern "C" {
 
@@ -689,6 +759,34 @@ hipError_t gsdrInt8FirFCAmDemodCarry(size_t decimation, const float* taps, size_
   if (e == hipSuccess) e = hipMemcpyAsync(carryIq, tmp, bytes, hipMemcpyDeviceToDevice, stream);
   const hipError_t f = hipFreeAsync(tmp, stream);
   return e != hipSuccess ? e : f;
+}
+
+hipError_t gsdrMixFirFC(size_t decimation, const float* taps, size_t tapCount, const hipFloatComplex* input,
+                        double phase0, double radiansPerSample, hipFloatComplex* output, size_t outputCount,
+                        int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInCF32, kEpiComplex>(input, taps, tapCount, decimation, output, outputCount, device,
+                                                 stream, mixSpec(phase0, radiansPerSample));
+}
+
+hipError_t gsdrMixFirFCAmDemod(size_t decimation, const float* taps, size_t tapCount, const hipFloatComplex* input,
+                               double phase0, double radiansPerSample, float* output, size_t outputCount,
+                               int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInCF32, kEpiAm>(input, taps, tapCount, decimation, output, outputCount, device, stream,
+                                            mixSpec(phase0, radiansPerSample));
+}
+
+hipError_t gsdrInt8MixFirFC(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
+                            double phase0, double radiansPerSample, hipFloatComplex* output, size_t outputCount,
+                            int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInI8IQ, kEpiComplex>(inputIq, taps, tapCount, decimation, output, outputCount, device,
+                                                 stream, mixSpec(phase0, radiansPerSample));
+}
+
+hipError_t gsdrInt8MixFirFCAmDemod(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
+                                   double phase0, double radiansPerSample, float* output, size_t outputCount,
+                                   int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInI8IQ, kEpiAm>(inputIq, taps, tapCount, decimation, output, outputCount, device, stream,
+                                            mixSpec(phase0, radiansPerSample));
 }
 
 hipError_t gsdrFirCCAmDemod(size_t decimation, const hipFloatComplex* taps, size_t tapCount,

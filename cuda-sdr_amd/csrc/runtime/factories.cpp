@@ -124,12 +124,19 @@ class QuadDemodFactory final : public IQuadDemodFactory {
     }
     IF_CATCH_RETURN_RESULT;
   }
+  // QuadDemodFactory.h:111 (same float expression)
+  static float quadDemodGain(float inputSampleRate, float fskDeviation) noexcept {
+    return inputSampleRate / (2.0f * 3.14159265358979323846f * fskDeviation * 5);
+  }
   Result<Filter> createQuadDemod(Modulation modulation, float rfSampleRate, float fskDeviation,
                                  ICudaCommandQueue* queue) noexcept final {
     if (modulation == Modulation_Am) return QuadAmDemod::create(queue, mF);
     if (modulation == Modulation_Fm) {
-      gsloge("QuadFmDemod %s", kOutOfScope);
-      return ERR_RESULT(Status_NotFound);
+      if (!(fskDeviation > 0.0f)) {
+        gsloge("FM demodulation needs fskDeviation > 0 (got %f)", fskDeviation);
+        return ERR_RESULT(Status_InvalidArgument);
+      }
+      return QuadFmDemod::create(quadDemodGain(rfSampleRate, fskDeviation), queue, mF);
     }
     gsloge("Modulation [%u] is not supported", modulation);
     return ERR_RESULT(Status_InvalidArgument);
@@ -348,7 +355,7 @@ class Factories final : public IFactories {
         mAddConstLen(new StubAddConstToVectorLengthFactory()),
         mFile(new StubFileReaderFactory()),
         mHackrf(new StubHackrfFactory()),
-        mMultiply(new StubQueueFilterFactory("MultiplyCCC")),
+        mMultiply(new QueueFilterFactory(this, &MultiplyCcc::create)),
         mStepping(new SteppingDriverFactory()),
         mComponent(new StubFilterDriverFactory()),
         mRemapSink(new StubPortRemappingSinkFactory()),

@@ -201,6 +201,124 @@ Status QuadAmDemod::readOutput(IBuffer** portOutputBuffers, size_t portCount) no
   return consumeInputBytesAndMoveUsedToStart(0, n * 2 * sizeof(float));
 }
 
+// ---- MultiplyCcc (Multiply.cpp:26-159) -------------------------------------------------------------------
+Result<Filter> MultiplyCcc::create(ICudaCommandQueue* queue, IFactories* factories) noexcept {
+  NON_NULL_PARAM_OR_RET(queue);
+  Ref<IRelocatableResizableBufferFactory> windows;
+  Ref<IMemSet> memSet;
+  UNWRAP_OR_FWD_RESULT(windows, factories->createRelocatableCudaBufferFactory(queue, 32, false));
+  UNWRAP_OR_FWD_RESULT(memSet, factories->getCudaMemSetFactory()->create(queue));
+  std::vector<ImmutableRef<IBufferCopier>> copiers;
+  UNWRAP_MOVE_OR_FWD_RESULT(copiers, deviceOutputCopiers(factories, queue));
+  return makeRefResultNonNull<Filter>(new (std::nothrow) MultiplyCcc(
+      queue, windows.get().get(), factories->getBufferSliceFactory(), memSet.get().get(), std::move(copiers)));
+}
+
+MultiplyCcc::MultiplyCcc(ICudaCommandQueue* queue, IRelocatableResizableBufferFactory* windows,
+                         IBufferSliceFactory* slices, IMemSet* memSet,
+                         std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept
+    : BaseFilter(windows, slices, 2, std::move(outputCopiers), memSet), mQueue(queue) {}
+
+// Multiply.cpp:63-76: the common prefix of both inputs
+size_t MultiplyCcc::availableElements() const noexcept {
+  if (!inputPortsInitialized()) return 0;
+  Result<const IBuffer> a = getPortInputBuffer(0);
+  Result<const IBuffer> b = getPortInputBuffer(1);
+  if (a.status != Status_Success || b.status != Status_Success) return 0;
+  return std::min(a.value->range()->used(), b.value->range()->used()) / sizeof(hipFloatComplex);
+}
+
+size_t MultiplyCcc::getOutputDataSize(size_t port) noexcept {
+  GS_REQUIRE_OR_RET_FMT(port == 0, 0, "Port [%zu] is out of range", port);
+  return availableElements() * sizeof(hipFloatComplex);
+}
+
+size_t MultiplyCcc::getOutputSizeAlignment(size_t port) noexcept {
+  GS_REQUIRE_OR_RET_FMT(port == 0, 0, "Output port [%zu] is out of range", port);
+  return 32 * sizeof(hipFloatComplex);
+}
+
+// Multiply.cpp:82-121: ask the lagging port for the difference (capped at 100 MiB), the leading
+// one for nothing; 8192 elements while both are empty.
+size_t MultiplyCcc::preferredInputBufferSize(size_t port) noexcept {
+  GS_REQUIRE_OR_RET_FMT(port <= 1, 0, "Input port [%zu] is out of range", port);
+  constexpr size_t kEmpty = 8192 * sizeof(hipFloatComplex);
+  if (!inputPortsInitialized()) return kEmpty;
+  Result<IBuffer> a = getPortInputBuffer(0);
+  Result<IBuffer> b = getPortInputBuffer(1);
+  if (a.status != Status_Success || b.status != Status_Success) return 0;
+  const size_t u0 = a.value->range()->used(), u1 = b.value->range()->used();
+  constexpr size_t kMax = 100 << 20;
+  if (u0 == 0 && u1 == 0) return kEmpty;
+  if (u0 >= u1) return port == 0 ? 0 : std::min(kMax, u0 - u1);
+  return port == 0 ? std::min(kMax, u1 - u0) : 0;
+}
+
+Status MultiplyCcc::readOutput(IBuffer** portOutputBuffers, size_t portCount) noexcept {
+  GS_REQUIRE_OR_RET_STATUS(portCount != 0 && portOutputBuffers != nullptr && portOutputBuffers[0] != nullptr,
+                           "One output port is required");
+  IBuffer* out = portOutputBuffers[0];
+  const size_t n = std::min(availableElements(), out->range()->remaining() / sizeof(hipFloatComplex));
+  if (n == 0) return Status_Success;
+  Ref<IBuffer> a, b;
+  UNWRAP_OR_FWD_STATUS(a, getPortInputBuffer(0));
+  UNWRAP_OR_FWD_STATUS(b, getPortInputBuffer(1));
+  // the reference ignores this status (Multiply.cpp:145, Appendix A): checked here
+  SAFE_HIP_OR_RET_STATUS(gsdrMultiplyCC(a->readPtr<hipFloatComplex>(), b->readPtr<hipFloatComplex>(),
+                                        out->writePtr<hipFloatComplex>(), n, mQueue->cudaDevice(),
+                                        mQueue->cudaStream()));
+  const size_t bytes = n * sizeof(hipFloatComplex);
+  FWD_IF_ERR(out->range()->increaseEndOffset(bytes));
+  FWD_IF_ERR(consumeInputBytesAndMoveUsedToStart(0, bytes));
+  return consumeInputBytesAndMoveUsedToStart(1, bytes);
+}
+
+// ---- QuadFmDemod (QuadFmDemod.cpp:28-115) -----------------------------------------------------------------
+Result<Filter> QuadFmDemod::create(float gain, ICudaCommandQueue* queue, IFactories* factories) noexcept {
+  NON_NULL_PARAM_OR_RET(queue);
+  Ref<IRelocatableResizableBufferFactory> windows;
+  Ref<IMemSet> memSet;
+  UNWRAP_OR_FWD_RESULT(windows, factories->createRelocatableCudaBufferFactory(queue, 32, false));
+  UNWRAP_OR_FWD_RESULT(memSet, factories->getCudaMemSetFactory()->create(queue));
+  std::vector<ImmutableRef<IBufferCopier>> copiers;
+  UNWRAP_MOVE_OR_FWD_RESULT(copiers, deviceOutputCopiers(factories, queue));
+  return makeRefResultNonNull<Filter>(new (std::nothrow) QuadFmDemod(
+      gain, queue, windows.get().get(), factories->getBufferSliceFactory(), memSet.get().get(), std::move(copiers)));
+}
+
+QuadFmDemod::QuadFmDemod(float gain, ICudaCommandQueue* queue, IRelocatableResizableBufferFactory* windows,
+                         IBufferSliceFactory* slices, IMemSet* memSet,
+                         std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept
+    : BaseFilter(windows, slices, 1, std::move(outputCopiers), memSet), mQueue(queue), mGain(gain) {}
+
+size_t QuadFmDemod::getOutputDataSize(size_t port) noexcept {
+  GS_REQUIRE_OR_RET_FMT(port == 0, 0, "Output port [%zu] is out of range", port);
+  Result<IBuffer> in = getPortInputBuffer(0);
+  if (in.status != Status_Success) return 0;
+  const size_t n = in.value->range()->used() / sizeof(hipFloatComplex);
+  return (n == 0 ? 0 : n - 1) * sizeof(float);
+}
+
+size_t QuadFmDemod::getOutputSizeAlignment(size_t port) noexcept {
+  GS_REQUIRE_OR_RET_FMT(port == 0, 0, "Output port [%zu] is out of range", port);
+  return 32 * sizeof(float);
+}
+
+Status QuadFmDemod::readOutput(IBuffer** portOutputBuffers, size_t portCount) noexcept {
+  GS_REQUIRE_OR_RET_STATUS(portCount != 0 && portOutputBuffers != nullptr && portOutputBuffers[0] != nullptr,
+                           "One output port is required");
+  IBuffer* out = portOutputBuffers[0];
+  Ref<IBuffer> in;
+  UNWRAP_OR_FWD_STATUS(in, getPortInputBuffer(0));
+  const size_t avail = in->range()->used() / sizeof(hipFloatComplex);
+  const size_t n = std::min(avail == 0 ? 0 : avail - 1, out->range()->remaining() / sizeof(float));
+  if (n == 0) return Status_Success;
+  SAFE_HIP_OR_RET_STATUS(gsdrQuadFmDemod(in->readPtr<hipFloatComplex>(), out->writePtr<float>(), mGain, n,
+                                         mQueue->cudaDevice(), mQueue->cudaStream()));
+  FWD_IF_ERR(out->range()->increaseEndOffset(n * sizeof(float)));
+  return consumeInputBytesAndMoveUsedToStart(0, n * sizeof(hipFloatComplex));
+}
+
 // ---- Int8ToFloat (Int8ToFloat.cpp:32-102) ----------------------------------------------------------------
 Result<Filter> Int8ToFloat::create(ICudaCommandQueue* queue, IFactories* factories) noexcept {
   NON_NULL_PARAM_OR_RET(queue);

@@ -65,6 +65,43 @@ class QuadAmDemod final : public BaseFilter {
   REF_COUNTED(QuadAmDemod);
 };
 
+// Two-input complex multiply (Multiply.cpp:26-159): the frequency shifter's mixer when port 1 is
+// fed by a ComplexCosine source.
+class MultiplyCcc final : public BaseFilter {
+ public:
+  static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
+  size_t getOutputDataSize(size_t port) noexcept final;
+  size_t getOutputSizeAlignment(size_t port) noexcept final;
+  Status readOutput(IBuffer** portOutputBuffers, size_t portCount) noexcept final;
+  size_t preferredInputBufferSize(size_t port) noexcept final;
+
+ private:
+  MultiplyCcc(ICudaCommandQueue* queue, IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
+              IMemSet* memSet, std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept;
+  size_t availableElements() const noexcept;
+  ConstRef<ICudaCommandQueue> mQueue;
+  REF_COUNTED(MultiplyCcc);
+};
+
+// Quadrature FM discriminator (QuadFmDemod.cpp:28-115): n inputs -> n - 1 outputs, the last input
+// kept for the next call.
+class QuadFmDemod final : public BaseFilter {
+ public:
+  static Result<Filter> create(float gain, ICudaCommandQueue* queue, IFactories* factories) noexcept;
+  size_t getOutputDataSize(size_t port) noexcept final;
+  size_t getOutputSizeAlignment(size_t port) noexcept final;
+  Status readOutput(IBuffer** portOutputBuffers, size_t portCount) noexcept final;
+  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+
+ private:
+  QuadFmDemod(float gain, ICudaCommandQueue* queue, IRelocatableResizableBufferFactory* windows,
+              IBufferSliceFactory* slices, IMemSet* memSet,
+              std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept;
+  ConstRef<ICudaCommandQueue> mQueue;
+  const float mGain;
+  REF_COUNTED(QuadFmDemod);
+};
+
 class Int8ToFloat final : public BaseFilter {
  public:
   static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;

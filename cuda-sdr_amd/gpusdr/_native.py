@@ -55,6 +55,14 @@ def _declare(L):
         fn = getattr(L, name)
         fn.argtypes = [f32, f32, vp, sz, i32, vp]
         fn.restype = err
+    for name in ("gsdrMixFirFC", "gsdrMixFirFCAmDemod", "gsdrInt8MixFirFC", "gsdrInt8MixFirFCAmDemod"):
+        fn = getattr(L, name)
+        fn.argtypes = [sz, vp, sz, vp, f64, f64, vp, sz, i32, vp]
+        fn.restype = err
+    L.gsdrMultiplyCC.argtypes = [vp, vp, vp, sz, i32, vp]
+    L.gsdrMultiplyCC.restype = err
+    L.gsdrQuadFmDemod.argtypes = [vp, vp, f32, sz, i32, vp]
+    L.gsdrQuadFmDemod.restype = err
     L.gsdrSynthIqInt8.argtypes = [u64, f64, f64, f64, u64, vp, sz, i32, vp]
     L.gsdrSynthIqInt8.restype = err
     L.gsdrSynthWidebandCf32.argtypes = [u64, f64, f64, u64, vp, sz, i32, vp]

@@ -44,6 +44,7 @@ def _L():
             "gspInt8ToFloatCreate": ([h, ph], u32),
             "gspCosineSourceCreate": ([u32, ctypes.c_float, ctypes.c_float, h, ph], u32),
             "gspNamedQueueCreate": ([ctypes.c_char_p, ctypes.c_char_p], u32),
+            "gspNamedQueueGet": ([ctypes.c_char_p, ph], u32),
             "gspNodeCreate": ([ctypes.c_char_p, ctypes.c_char_p, ph], u32),
             "gspSinkPushHost": ([h, sz, vp, sz, h], u32),
             "gspSinkPushDevice": ([h, sz, vp, sz, h], u32),
@@ -104,8 +105,16 @@ def _create(fn, *args, what=""):
 class Queue(_Handle):
     """ICudaCommandQueue: one HIP device + one non-blocking stream."""
 
-    def __init__(self, device: int = 0):
-        super().__init__(_create(_L().gspQueueCreate, device, what="gspQueueCreate"))
+    def __init__(self, device: int = 0, _ptr=None):
+        super().__init__(_ptr if _ptr is not None else _create(_L().gspQueueCreate, device, what="gspQueueCreate"))
+
+    @classmethod
+    def named(cls, name: str, device: int = 0) -> "Queue":
+        """Create (or reuse) the named queue JSON nodes refer to ({"commandQueue": name})."""
+        st = _L().gspNamedQueueCreate(name.encode(), f'{{"queueType": "hip", "cudaDevice": {device}}}'.encode())
+        if st not in (0, 5):  # Status_InvalidState: the name exists already
+            _check(st, "gspNamedQueueCreate")
+        return cls(_ptr=_create(_L().gspNamedQueueGet, name.encode(), what="gspNamedQueueGet"))
 
     @property
     def stream(self) -> int:

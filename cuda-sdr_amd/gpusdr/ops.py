@@ -51,12 +51,19 @@ _FIR_ENTRY = {
 }
 
 
+_MIX_ENTRY = {("c64", False): "gsdrMixFirFC", ("c64", True): "gsdrMixFirFCAmDemod",
+              ("i8iq", False): "gsdrInt8MixFirFC", ("i8iq", True): "gsdrInt8MixFirFCAmDemod"}
+
+
 def fir(taps: torch.Tensor, x: torch.Tensor, decimation: int = 1, num_outputs: int | None = None,
-        out: torch.Tensor | None = None, am: bool = False, int8_iq: bool = False) -> torch.Tensor:
+        out: torch.Tensor | None = None, am: bool = False, int8_iq: bool = False,
+        mix: tuple[float, float] | None = None) -> torch.Tensor:
     """y[k] = sum_j taps[j] * x[k*D + j] on the GPU.
 
     taps: float32 (real) or complex64, device.  x: float32, complex64, or (int8_iq=True) int8
-    interleaved I/Q.  am=True fuses the QuadAmDemod envelope (float32 output)."""
+    interleaved I/Q.  am=True fuses the QuadAmDemod envelope (float32 output).
+    mix=(phase0, radians_per_sample): frequency-shift the (complex) input first, fused into the
+    load (gsdr*MixFirFC*; real taps only)."""
     taps_c = taps.dtype == torch.complex64
     _require(taps, torch.complex64 if taps_c else torch.float32, "taps")
     if int8_iq:
@@ -85,6 +92,13 @@ def fir(taps: torch.Tensor, x: torch.Tensor, decimation: int = 1, num_outputs: i
         if out.numel() < num_outputs:
             raise ValueError("out too small")
     if num_outputs == 0:
+        return out
+    if mix is not None:
+        if taps_c or kind == "f32":
+            raise ValueError("mix needs real taps and complex input")
+        fn = getattr(lib(), _MIX_ENTRY[(kind, am)])
+        check(fn(d, taps.data_ptr(), T, x.data_ptr(), float(mix[0]), float(mix[1]), out.data_ptr(), num_outputs,
+                 _dev(x), _stream(x)), fn.__name__)
         return out
     fn = getattr(lib(), _FIR_ENTRY[key])
     check(fn(d, taps.data_ptr(), T, x.data_ptr(), out.data_ptr(), num_outputs, _dev(x), _stream(x)), fn.__name__)
@@ -116,6 +130,28 @@ def quad_am_demod(z: torch.Tensor, out: torch.Tensor | None = None) -> torch.Ten
     if out is None:
         out = torch.empty(z.numel(), dtype=torch.float32, device=z.device)
     check(lib().gsdrQuadAmDemod(z.data_ptr(), out.data_ptr(), z.numel(), _dev(z), _stream(z)), "gsdrQuadAmDemod")
+    return out
+
+
+def multiply_cc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """gsdrMultiplyCC: element-wise non-conjugate complex product (MultiplyCcc)."""
+    _require(a, torch.complex64, "a")
+    _require(b, torch.complex64, "b")
+    n = min(a.numel(), b.numel())
+    if out is None:
+        out = torch.empty(n, dtype=torch.complex64, device=a.device)
+    check(lib().gsdrMultiplyCC(a.data_ptr(), b.data_ptr(), out.data_ptr(), n, _dev(a), _stream(a)), "gsdrMultiplyCC")
+    return out
+
+
+def quad_fm_demod(z: torch.Tensor, gain: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    """gsdrQuadFmDemod: len(z) - 1 outputs gain * arg(z[i+1] conj(z[i]))."""
+    _require(z, torch.complex64, "z")
+    n = max(z.numel() - 1, 0)
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=z.device)
+    check(lib().gsdrQuadFmDemod(z.data_ptr(), out.data_ptr(), float(gain), n, _dev(z), _stream(z)),
+          "gsdrQuadFmDemod")
     return out
 
 

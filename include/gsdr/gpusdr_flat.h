@@ -52,6 +52,8 @@ GSP_API uint32_t gspInt8ToFloatCreate(gspHandle queue, gspHandle* filterOut);
 GSP_API uint32_t gspCosineSourceCreate(uint32_t sampleType, float sampleRate, float frequency, gspHandle queue,
                                        gspHandle* sourceOut);
 GSP_API uint32_t gspNamedQueueCreate(const char* queueId, const char* json);
+/* The queue a JSON node refers to by name (ICommandQueueFactory::getCudaCommandQueue). */
+GSP_API uint32_t gspNamedQueueGet(const char* queueId, gspHandle* queueOut);
 GSP_API uint32_t gspNodeCreate(const char* name, const char* json, gspHandle* nodeOut);
 
 /* Sink side of a filter node: append host bytes to input port `port`. */

@@ -84,6 +84,23 @@ GSDR_API hipError_t gsdrCosineF(float phiBegin, float phiEnd, float* output, siz
 GSDR_API hipError_t gsdrCosineC(float phiBegin, float phiEnd, hipFloatComplex* output, size_t numElements,
                                 int32_t device, hipStream_t stream);
 
+/*
+ * Complex multiply (Multiply.cpp:145, MultiplyCcc::readOutput), non-conjugate:
+ *     out[i] = { fmaf(a.re, b.re, -(a.im * b.im)), fmaf(a.re, b.im, a.im * b.re) }
+ * The expression is this build's definition (gsdr is absent); the oracle uses the same one.
+ */
+GSDR_API hipError_t gsdrMultiplyCC(const hipFloatComplex* a, const hipFloatComplex* b, hipFloatComplex* output,
+                                   size_t numElements, int32_t device, hipStream_t stream);
+
+/*
+ * Quadrature FM discriminator (QuadFmDemod.cpp:80-115): numOutputs = inputs - 1,
+ *     p = input[i + 1] * conj(input[i]) = { fmaf(r1, r0, i1 * i0), fmaf(i1, r0, -(r1 * i0)) }
+ *     output[i] = gain * atan2f(p.im, p.re)
+ * with gain = sampleRate / (2 pi fskDeviation 5) from QuadDemodFactory (QuadDemodFactory.h:111).
+ */
+GSDR_API hipError_t gsdrQuadFmDemod(const hipFloatComplex* input, float* output, float gain, size_t numOutputs,
+                                    int32_t device, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,6 +48,28 @@ GSDR_API hipError_t gsdrInt8FirFCAmDemodCarry(size_t decimation, const float* ta
                                               int8_t* carryIq, int32_t device, hipStream_t stream);
 
 /*
+ * Frequency shifter fused into the FIR input load (the reference's
+ * ComplexCosineSource -> MultiplyCcc -> Fir front end, RfToPcmAudioFactory.cpp:218-235): input
+ * sample n (n = 0 at `input`) is multiplied by exp(j theta(n)) before the FIR,
+ *     theta(n) = phase0 + n * radiansPerSample,
+ * reduced exactly modulo 2 pi (64-bit fixed-point cycle fractions) and then evaluated in float
+ * (sincosf); the product is the gsdrMultiplyCC expression. A streaming caller advances phase0 by
+ * consumed * radiansPerSample (mod 2 pi) between calls. No tone is materialised in HBM.
+ */
+GSDR_API hipError_t gsdrMixFirFC(size_t decimation, const float* taps, size_t tapCount, const hipFloatComplex* input,
+                                 double phase0, double radiansPerSample, hipFloatComplex* output, size_t outputCount,
+                                 int32_t device, hipStream_t stream);
+GSDR_API hipError_t gsdrMixFirFCAmDemod(size_t decimation, const float* taps, size_t tapCount,
+                                        const hipFloatComplex* input, double phase0, double radiansPerSample,
+                                        float* output, size_t outputCount, int32_t device, hipStream_t stream);
+GSDR_API hipError_t gsdrInt8MixFirFC(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
+                                     double phase0, double radiansPerSample, hipFloatComplex* output,
+                                     size_t outputCount, int32_t device, hipStream_t stream);
+GSDR_API hipError_t gsdrInt8MixFirFCAmDemod(size_t decimation, const float* taps, size_t tapCount,
+                                            const int8_t* inputIq, double phase0, double radiansPerSample,
+                                            float* output, size_t outputCount, int32_t device, hipStream_t stream);
+
+/*
  * Deterministic synthetic sources for the benchmark configurations.
  * Sample n (absolute stream index firstSample + i) depends only on (seed, n), so a
  * time-sharded stream is generated shard by shard with no communication.

@@ -62,6 +62,27 @@ void orc_quad_am_demod(const float* inComplex, float* out, size_t n) {
   for (size_t i = 0; i < n; ++i) out[i] = am_envelope(inComplex[2 * i], inComplex[2 * i + 1]);
 }
 
+/* include/gsdr/gsdr.h gsdrMultiplyCC (Multiply.cpp:145): non-conjugate complex product. */
+void orc_multiply_cc(const float* a, const float* b, float* out, size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    const float ar = a[2 * i], ai = a[2 * i + 1], br = b[2 * i], bi = b[2 * i + 1];
+    out[2 * i] = fmaf(ar, br, -(ai * bi));
+    out[2 * i + 1] = fmaf(ar, bi, ai * br);
+  }
+}
+
+/* include/gsdr/gsdr.h gsdrQuadFmDemod (QuadFmDemod.cpp:80-115): the float32 discriminator product
+ * exactly as the kernel forms it, then gain * atan2 in float64 (the kernel's atan2f is checked
+ * against this within its ulp bound). */
+void orc_quad_fm_demod_f64(const float* in, double gain, double* out, size_t nOut) {
+  for (size_t i = 0; i < nOut; ++i) {
+    const float r0 = in[2 * i], i0 = in[2 * i + 1], r1 = in[2 * i + 2], i1 = in[2 * i + 3];
+    const float re = fmaf(r1, r0, i1 * i0);
+    const float im = fmaf(i1, r0, -(r1 * i0));
+    out[i] = gain * atan2((double)im, (double)re);
+  }
+}
+
 /* CosineSource.cpp:70-83: the source passes (phi, phi + n * delta) and the kernel spreads
  * the phase linearly over n samples. */
 void orc_cosine_f(float phiBegin, float phiEnd, float* out, size_t n) {

@@ -56,6 +56,8 @@ def lib():
         L.orc_int8_to_norm.restype = f32
         L.orc_int8_to_float.argtypes = [vp, vp, sz]
         L.orc_quad_am_demod.argtypes = [vp, vp, sz]
+        L.orc_multiply_cc.argtypes = [vp, vp, vp, sz]
+        L.orc_quad_fm_demod_f64.argtypes = [vp, f64, vp, sz]
         L.orc_cosine_f.argtypes = [f32, f32, vp, sz]
         L.orc_cosine_c.argtypes = [f32, f32, vp, sz]
         L.orc_synth_iq_int8.argtypes = [u64, f64, f64, f64, u64, vp, sz]
@@ -113,6 +115,47 @@ def quad_am_demod(z: np.ndarray) -> np.ndarray:
     out = np.empty(len(zz), dtype=np.float32)
     lib().orc_quad_am_demod(_ptr(zz), _ptr(out), len(zz))
     return out
+
+
+def multiply_cc(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """gsdrMultiplyCC restated (Multiply.cpp:145): non-conjugate product, bit-exact."""
+    aa = np.ascontiguousarray(a, dtype=np.complex64)
+    bb = np.ascontiguousarray(b, dtype=np.complex64)
+    out = np.empty(max(len(aa), 1), dtype=np.complex64)
+    lib().orc_multiply_cc(_ptr(aa), _ptr(bb), _ptr(out), len(aa))
+    return out[: len(aa)]
+
+
+def quad_fm_demod_f64(z: np.ndarray, gain: float) -> np.ndarray:
+    """gsdrQuadFmDemod restated (QuadFmDemod.cpp:80-115): len(z) - 1 outputs; the float32
+    product as the kernel forms it, atan2 in float64."""
+    zz = np.ascontiguousarray(z, dtype=np.complex64)
+    n = max(len(zz) - 1, 0)
+    out = np.empty(max(n, 1), dtype=np.float64)
+    lib().orc_quad_fm_demod_f64(_ptr(zz), float(gain), _ptr(out), n)
+    return out[:n]
+
+
+def mix_phase_fraction(rad: float) -> int:
+    """Radians -> the 64-bit cycle fraction the fused mixer uses (include/gsdr/gsdr_amd.h)."""
+    import math
+    c = rad / 6.283185307179586476925286766559
+    c -= math.floor(c)
+    return int(math.ldexp(c, 64))
+
+
+def mix_f64(x: np.ndarray, phase0: float, step: float) -> np.ndarray:
+    """The fused frequency shifter restated: sample n times exp(j theta(n)), theta(n) the float32
+    value of 2 pi (P0 + n F mod 2^64) / 2^64 (signed), the exponential in float64."""
+    n = np.arange(len(x), dtype=np.uint64)
+    ph = np.uint64(mix_phase_fraction(phase0)) + n * np.uint64(mix_phase_fraction(step))  # wraps mod 2^64
+    th = (ph.view(np.int64).astype(np.float64) * 3.4061215800865545e-19).astype(np.float32)
+    return np.asarray(x, dtype=np.complex128) * np.exp(1j * th.astype(np.float64))
+
+
+def fm_gain(sample_rate: float, fsk_deviation: float) -> float:
+    """QuadDemodFactory.h:111 (float arithmetic as in the reference)."""
+    return float(np.float32(sample_rate) / (np.float32(2.0) * np.float32(np.pi) * np.float32(fsk_deviation) * np.float32(5)))
 
 
 def cosine_f(phi_begin: float, phi_end: float, n: int) -> np.ndarray:

@@ -136,7 +136,11 @@ void jsonRegistry() {
   firTwoCommits(fir.get(), q.get());
   Result<Filter> fm = createFilter("QuadDemod", R"({"commandQueue": "kat", "modulation": "fm", "sampleRate": 1e6,
                                                     "fskDeviation": 5e3})");
-  CHECK(fm.status == Status_NotFound);  // FM is outside this build's scope
+  CHECK(fm.status == Status_Success && fm.value != nullptr);  // QuadFmDemod (QuadDemodFactory.h:91-110)
+  if (fm.value != nullptr) fm.value->unref();
+  Result<Filter> mul = createFilter("MultiplyCCC", R"({"commandQueue": "kat"})");
+  CHECK(mul.status == Status_Success && mul.value != nullptr);
+  if (mul.value != nullptr) mul.value->unref();
   ConstRef<Filter> am = unwrap(createFilter("QuadDemod", R"({"commandQueue": "kat", "modulation": "am"})"));
   CHECK(static_cast<Node*>(am.get())->asFilter() != nullptr);
   Result<Filter> bad = createFilter("Fir", "{not json");

@@ -121,13 +121,13 @@ def test_cosine_source_phase_continuity(graph, queue, orc):
 def test_json_nodes_and_out_of_scope(graph, queue):
     from gpusdr._native import lib
     import ctypes
-    assert graph._L().gspNamedQueueCreate(b"q0", b'{"queueType": "hip", "cudaDevice": 0}') == 0
+    queue = graph.Queue.named("q0")  # the node's own stream for pushes and reads
     fir = graph.Node.from_json("Fir", '{"commandQueue": "q0", "taps": [0.5, 1.0], "tapType": "Float", '
                                       '"elementType": "FloatComplex", "decimation": 2}', queue)
     fir.push(np.array([0.1 + 0.2j, 0.3 + 0.4j, 0.5 + 0.6j, 0.7 + 0.8j, 0.9 + 0.9j], np.complex64))
     y = _drain(graph, queue, fir, 64, np.complex64)
     assert np.allclose(y, [0.35 + 0.5j, 0.95 + 1.1j], atol=1e-6)
-    for name in ("MultiplyCCC", "HackRfSource", "AacWriter"):
+    for name in ("HackRfSource", "AacWriter"):
         with pytest.raises(graph.GraphError) as e:
             graph.Node.from_json(name, '{"commandQueue": "q0"}')
         assert e.value.status == 8  # Status_NotFound
@@ -176,3 +176,99 @@ def test_stepping_driver_am_chain(graph, queue, orc, T, D):
     assert len(got) == len(want) > 0
     # AM of an FIR output: the FIR bound plus the sqrt rounding (AM_TOL relative)
     assert np.all(np.abs(got - want) <= FIR_TOL * bound + 1e-6 * want + 1e-30)
+
+
+
+def test_multiply_filter_bit_exact(graph, queue, orc):
+    """MultiplyCcc (Multiply.cpp:26-159): two ports filled unevenly, output = the common prefix,
+    bit-exact against the oracle product; preferredInputBufferSize asks the lagging port for
+    the difference."""
+    queue = graph.Queue.named("qm")  # pushes and reads on the node's own stream
+    mul = graph.Node.from_json("MultiplyCCC", '{"commandQueue": "qm"}', queue)
+    rng = np.random.default_rng(4)
+    a = (rng.standard_normal(5000) + 1j * rng.standard_normal(5000)).astype(np.complex64)
+    b = (rng.standard_normal(5000) + 1j * rng.standard_normal(5000)).astype(np.complex64)
+    assert mul.preferred_input_size(0) == 8192 * 8
+    mul.push(a[:3000], port=0)
+    mul.push(b[:1000], port=1)
+    assert mul.preferred_input_size(0) == 0 and mul.preferred_input_size(1) == 2000 * 8
+    assert mul.output_size()[0] == 1000 * 8
+    got = [_drain(graph, queue, mul, 700 * 8, np.complex64)]
+    mul.push(a[3000:], port=0)
+    mul.push(b[1000:], port=1)
+    got.append(_drain(graph, queue, mul, 5000 * 8, np.complex64))
+    got = np.concatenate(got)
+    assert got.tobytes() == orc.multiply_cc(a, b).tobytes()
+
+
+def test_quad_fm_demod_filter(graph, queue, orc):
+    """QuadFmDemod (QuadFmDemod.cpp:80-115): n inputs give n - 1 outputs, the last input is kept,
+    so chunked reads equal the whole-stream discriminator; gain from QuadDemodFactory.h:111."""
+    queue = graph.Queue.named("qf")
+    fs, dev = 240000.0, 75000.0
+    fm = graph.Node.from_json("QuadDemod", f'{{"commandQueue": "qf", "modulation": "fm", "sampleRate": {fs}, '
+                                           f'"fskDeviation": {dev}}}', queue)
+    gain = orc.fm_gain(fs, dev)
+    rng = np.random.default_rng(8)
+    n = 20000
+    phase = np.cumsum(rng.uniform(-2.5, 2.5, n))
+    z = (np.exp(1j * phase) * rng.uniform(0.5, 2.0, n)).astype(np.complex64)
+    got, pos = [], 0
+    for c in (1, 2, 777, 5000, 14220):
+        fm.push(z[pos: pos + c])
+        pos += c
+        size, _ = fm.output_size()
+        got.append(_drain(graph, queue, fm, max(size, 4), np.float32))
+    got = np.concatenate(got)
+    want = orc.quad_fm_demod_f64(z, gain)
+    assert len(got) == n - 1
+    # atan2f within 2 ulp of the float64 angle of the same float32 product
+    assert np.all(np.abs(got - want) <= abs(gain) * (4 * np.spacing(np.float32(np.pi))) + 2 * np.spacing(np.abs(want).astype(np.float32)))
+
+
+def test_frequency_shifter_fm_chain(graph, queue, orc):
+    """The reference's FM front (RfToPcmAudioFactory.cpp:218-235): ComplexCosine -> MultiplyCcc
+    port 1, IQ pushed into port 0 from outside, -> Fir (D=4) -> QuadFmDemod, stepped by the
+    SteppingDriver. The driver pulls exactly the cosine samples the mixer lacks (the lagging port's
+    preferred size), so the mixer sees one phase-continuous tone; the output is compared with the
+    oracle chain over the whole stream."""
+    queue = graph.Queue.named("qs")  # every node on one stream: pushes, kernels and reads ordered
+    fs, shift, dev, D, T = 1.0e6, -150000.0, 75000.0, 4, 127
+    cos = graph.Node.cosine(queue, graph.SAMPLE_FLOAT_COMPLEX, fs, shift)
+    mul = graph.Node.from_json("MultiplyCCC", '{"commandQueue": "qs"}', queue)
+    taps = orc.lowpass_taps(T, 0.1)
+    fir = graph.Node.fir(queue, taps, D, graph.SAMPLE_FLOAT_COMPLEX)
+    fm = graph.Node.from_json("QuadDemod", f'{{"commandQueue": "qs", "modulation": "fm", "sampleRate": {fs / D}, '
+                                           f'"fskDeviation": {dev}}}', queue)
+    drv = graph.SteppingDriver()
+    drv.connect(cos, 0, mul, 1)
+    drv.connect(mul, 0, fir, 0)
+    drv.connect(fir, 0, fm, 0)
+    rng = np.random.default_rng(21)
+    n = 300000
+    t = np.arange(n)
+    msg = np.cumsum(0.3 * np.sin(2 * np.pi * 1e3 * t / fs))
+    x = (np.exp(1j * (2 * np.pi * 150000.0 * t / fs + msg)) + 0.01 * rng.standard_normal(n)).astype(np.complex64)
+    got, pos = [], 0
+    for c in (50000, 1, 99999, 150000):
+        mul.push(x[pos: pos + c], port=0)
+        pos += c
+        for _ in range(16):
+            drv.do_filter()
+        size, _ = fm.output_size()
+        got.append(_drain(graph, queue, fm, max(size, 4), np.float32))
+    got = np.concatenate(got)
+    # oracle: the tone exp(j 2 pi shift i / fs), the mixer, the FIR in float64, the discriminator
+    tone = np.exp(1j * 2 * np.pi * shift * t / fs)
+    y, bound = orc.fir_f64(taps, (x * tone).astype(np.complex64), D)
+    want = orc.fm_gain(fs / D, dev) * np.angle(y[1:] * np.conj(y[:-1]))
+    assert len(got) == len(want)
+    # The source forms phi_i = phi + i * step in float32 over a whole readOutput chunk before
+    # reducing mod 2 pi (CosineSource.cpp:74-82, the reference's arithmetic, kept): with chunks of
+    # up to 1 MiB the phase reaches ~1.2e5 rad, whose float spacing (7.8e-3 rad) is per-sample
+    # phase noise of the tone. The FIR averages it; the discriminator keeps ~1e-3 rad of it
+    # (a few outputs up to ~2e-2 where the spacing noise of neighbouring samples adds up).
+    g = abs(orc.fm_gain(fs / D, dev))
+    err = np.abs(got - want) / g
+    assert np.median(err) <= 1e-3
+    assert np.max(err) <= 5e-2, (int(np.argmax(err)), float(np.max(err)))

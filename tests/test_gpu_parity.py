@@ -419,3 +419,56 @@ def test_graph_capture_replay(ops, orc):
     x = orc.int8_to_float(_host(iq)).view(np.complex64)
     y64, bound = orc.fir_f64(_host(taps), x, D, n_out)
     assert np.all(np.abs(_host(out) - np.abs(y64)) <= FIR_TOL * bound)
+
+
+def test_multiply_cc_bit_exact(ops, orc):
+    rng = np.random.default_rng(31)
+    for n in (1, 7, 4096, 100003):
+        a = (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+        b = (rng.standard_normal(n) * 1e3 + 1j * rng.standard_normal(n)).astype(np.complex64)
+        got = _host(ops.multiply_cc(_dev(a), _dev(b)))
+        assert got.tobytes() == orc.multiply_cc(a, b).tobytes()
+
+
+def test_quad_fm_demod_kernel(ops, orc):
+    rng = np.random.default_rng(32)
+    gain = orc.fm_gain(2.4e5, 7.5e4)
+    for n in (2, 3, 1000, 65537):
+        z = ((rng.standard_normal(n) + 1j * rng.standard_normal(n)) * 10.0 ** rng.uniform(-3, 3, n)).astype(np.complex64)
+        got = _host(ops.quad_fm_demod(_dev(z), gain))
+        want = orc.quad_fm_demod_f64(z, gain)
+        assert len(got) == n - 1
+        assert np.all(np.abs(got - want) <= abs(gain) * 4 * np.spacing(np.float32(np.pi)) +
+                      2 * np.spacing(np.abs(want).astype(np.float32)))
+
+
+@pytest.mark.parametrize("kind,T,D,n_out", [("c64", 127, 1, 5000), ("c64", 1023, 10, 3000), ("i8", 127, 1, 70000),
+                                             ("i8", 1023, 10, 20000), ("c64", 64, 3, 1), ("i8", 255, 4, 777)])
+def test_fused_frequency_shift_fir(ops, orc, kind, T, D, n_out):
+    """Frequency shifter fused into the FIR load (gsdr*MixFirFC*): against the oracle mixer
+    (exact 64-bit phase, float32 angle, float64 exponential) and float64 FIR; the AM variant
+    against |y|; and streaming: two calls with phase0 advanced by the consumed samples equal one."""
+    rng = np.random.default_rng(T + D + n_out)
+    n_in = (n_out - 1) * D + T
+    phase0, step = 1.2345, -2 * np.pi * 0.15
+    taps = orc.lowpass_taps(T, 0.4 / D)
+    if kind == "c64":
+        x = (rng.standard_normal(n_in) + 1j * rng.standard_normal(n_in)).astype(np.complex64)
+        xd, xf = _dev(x), x
+    else:
+        iq = rng.integers(-128, 128, size=2 * n_in).astype(np.int8)
+        xd, xf = _dev(iq), orc.int8_to_float(iq).view(np.complex64)
+    td = _dev(taps)
+    y = _host(ops.fir(td, xd, D, n_out, int8_iq=(kind == "i8"), mix=(phase0, step)))
+    am = _host(ops.fir(td, xd, D, n_out, int8_iq=(kind == "i8"), am=True, mix=(phase0, step)))
+    mixed = orc.mix_f64(xf, phase0, step)
+    y64, bound = orc.fir_f64(taps, mixed.astype(np.complex64), D, n_out)
+    _check_fir(y, y64, bound, ("mix", kind, T, D))
+    assert np.all(np.abs(am - np.abs(y64)) <= FIR_TOL * bound + 1e-30)
+    if n_out >= 4:
+        h = n_out // 2
+        w = 2 if kind == "i8" else 1
+        y1 = _host(ops.fir(td, xd, D, h, int8_iq=(kind == "i8"), mix=(phase0, step)))
+        y2 = _host(ops.fir(td, xd[w * h * D:], D, n_out - h, int8_iq=(kind == "i8"),
+                           mix=(np.fmod(phase0 + h * D * step, 2 * np.pi), step)))
+        _check_fir(np.concatenate([y1, y2]), y64, bound, ("mix-stream", kind, T, D))
