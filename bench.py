@@ -164,7 +164,7 @@ class ShardedChain:
             return in_bytes + n * 4, n * 2 * 2 * 32 * s * 2  # I and Q rows x 2 f16 limbs x K MACs x 2
         if self.mfma_cf:
             ks = -(-(-(-(31 * self.D + self.T) // 16)) // 8)  # K-steps of 16 per wave, 8 waves
-            return in_bytes + n * 4, n * 2 * (8 * ks * 16) * 6 * 2  # I/Q rows x K x 6 bf16 products x 2
+            return in_bytes + n * 4, n * 2 * (8 * ks * 16) * 3 * 2  # I/Q rows x K x 3 f16 products x 2
         return in_bytes + n * 4, n * self.T * 4
 
     @property
@@ -271,7 +271,7 @@ def kernel_name(chain):
                 "HIP events around the whole step)")
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"
-    body = "firI8MfmaKernel" if chain.mfma_int8 else ("firCfMfmaKernel" if chain.mfma_cf else "firLdsKernel")
+    body = "firI8MfmaKernel" if chain.mfma_int8 else ("firCfF16MfmaKernel" if chain.mfma_cf else "firLdsKernel")
     return f"{entry} ({body})"
 
 
@@ -375,7 +375,7 @@ def main():
                 "compute": ({"kind": "f16 MFMA (2 tap limbs, fp32 accumulate)", "achieved_tflops": achieved_t,
                              "peak_tflops": F16_PEAK_TFLOPS, "frac": achieved_t / F16_PEAK_TFLOPS,
                              "flops_per_launch": ops_} if chain.mfma_int8 else
-                            {"kind": "bf16 MFMA (3x3 limb split, 6 products, fp32 accumulate)",
+                            {"kind": "f16 MFMA (2x2 limbs with per-tile scale, 3 products, fp32 accumulate)",
                              "achieved_tflops": achieved_t, "peak_tflops": F16_PEAK_TFLOPS,
                              "frac": achieved_t / F16_PEAK_TFLOPS, "flops_per_launch": ops_} if chain.mfma_cf else
                             {"kind": "fp32 VALU FMA", "achieved_tflops": achieved_t,

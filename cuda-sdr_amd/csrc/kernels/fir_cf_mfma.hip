@@ -35,10 +35,13 @@
 #include "kcommon.h"
 #include "fir_launch.h"
 
+#include <gsdr/gsdr_amd.h>
+
 namespace gsdr_amd {
 
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 #ifndef GSDR_CF_EXPERIMENT
@@ -279,6 +282,349 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
 }
 
 
+// ---- cf32 input on f16 limbs with a per-tile scale (default cf32 MFMA path) ---------------------
+//
+// x = x0 + x1 (two f16 limbs, RNE, after scaling the tile by 2^sx so that its largest component
+// lands in [2^14, 2^15)) and h = h0 + h1 (two f16 limbs, block scale 2^sh): the three products
+// x0 h0, x0 h1, x1 h0 carry every term down to 2^-22 of |x h| (the dropped x1 h1 and the limb
+// remainders are <= 2^-22 each), on v_mfma_f32_32x32x16_f16 - half the matrix work of the bf16 x 3
+// split and four planes instead of six. A fixed scale per tile keeps 22 bits for samples down to
+// 2^-16 of the tile's largest: a tile holding a non-finite sample, or a 64-sample block whose
+// largest magnitude is below 2^-16 of the tile's (a quiet stretch next to a loud one), takes the
+// direct fp32 path, so every output keeps its error relative to its OWN window
+// (test_cf_mfma_dynamic_range).
+
+// Window statistics of one tile, in two halves around a barrier the caller provides:
+// cfStatsLocal reduces the thread's units over the wave and leaves the wave's (max, smallest
+// nonzero 64-sample-block max) in red[.][wave]; cfStatsFinish reads all waves' after the barrier
+// and decides the tile's scale or the direct path.
+template <int G>
+__device__ __forceinline__ void cfStatsLocal(const CfFirArgs& a, const CfWindow<G>& w, int tid, float (*red)[kCfWaves]) {
+  const int lane = tid & (kWave - 1);
+  const int wave = tid >> 6;
+  float m = 0.0f;         // largest |component| of this thread's units
+  float bmin = INFINITY;  // smallest nonzero 64-sample-block maximum seen by this thread
+  f4 probe = f4{};
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int g = tid + kCfThreads * j;
+    float um = 0.0f;
+    if (g < a.Wu) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f4 v = w.v[j][q];
+        probe += v * 0.0f;
+        um = fmaxf(um, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
+    }
+    // 64-sample block = 8 consecutive units = 8 consecutive lanes
+    float bm = um;
+    bm = fmaxf(bm, __shfl_xor(bm, 1));
+    bm = fmaxf(bm, __shfl_xor(bm, 2));
+    bm = fmaxf(bm, __shfl_xor(bm, 4));
+    m = fmaxf(m, um);
+    if (bm > 0.0f) bmin = fminf(bmin, bm);
+  }
+  const float pr = (probe.x + probe.y) + (probe.z + probe.w);
+  if (pr != pr) m = INFINITY;  // non-finite sample: direct path
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    m = fmaxf(m, __shfl_xor(m, o));
+    bmin = fminf(bmin, __shfl_xor(bmin, o));
+  }
+  if (lane == 0) {
+    red[0][wave] = m;
+    red[1][wave] = bmin;
+  }
+}
+
+__device__ __forceinline__ bool cfStatsFinish(const float (*red)[kCfWaves], int* sxOut) {
+  float M = red[0][0], B = red[1][0];
+#pragma unroll
+  for (int v = 1; v < kCfWaves; ++v) {
+    M = fmaxf(M, red[0][v]);
+    B = fminf(B, red[1][v]);
+  }
+  *sxOut = 0;
+  if (!(M <= 3.0e38f)) return true;  // inf / NaN
+  if (M == 0.0f) return false;
+  if (M < 1.0e-30f || B < M * (1.0f / 65536.0f)) return true;  // would lose bits below 2^-22
+  *sxOut = 14 - ilogbf(M);
+  return false;
+}
+
+// Both halves with their own barriers (prologue and the single-set kernel).
+template <int G>
+__device__ __forceinline__ bool cfTileStats(const CfFirArgs& a, const CfWindow<G>& w, int tid, float (*red)[kCfWaves],
+                                            int* sxOut) {
+  cfStatsLocal<G>(a, w, tid, red);
+  __syncthreads();
+  const bool d = cfStatsFinish(red, sxOut);
+  __syncthreads();  // red[] is rewritten by the next tile's statistics
+  return d;
+}
+
+// Split group j of the thread's window into the four f16 planes (limb l, component c at 2 l + c).
+template <int G>
+__device__ __forceinline__ void splitGroupF16(const CfFirArgs& a, const CfWindow<G>& w, int8_t* planes, int tid,
+                                              float scale, int j) {
+  const int g = tid + kCfThreads * j;
+  if (g < a.Wu) {
+    h8 i0, i1, q0, q1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // samples 2q, 2q + 1: (re, im, re, im)
+      const f4 v = w.v[j][q] * scale;
+      const _Float16 a0 = (_Float16)v.x, b0 = (_Float16)v.y, c0 = (_Float16)v.z, d0 = (_Float16)v.w;
+      i0[2 * q] = a0;
+      i0[2 * q + 1] = c0;
+      q0[2 * q] = b0;
+      q0[2 * q + 1] = d0;
+      i1[2 * q] = (_Float16)(v.x - (float)a0);
+      i1[2 * q + 1] = (_Float16)(v.z - (float)c0);
+      q1[2 * q] = (_Float16)(v.y - (float)b0);
+      q1[2 * q + 1] = (_Float16)(v.w - (float)d0);
+    }
+    const int off = 16 * cfPhys(g, a.padShift);
+    *reinterpret_cast<h8*>(planes + off) = i0;
+    *reinterpret_cast<h8*>(planes + a.planeStride + off) = q0;
+    *reinterpret_cast<h8*>(planes + 2 * a.planeStride + off) = i1;
+    *reinterpret_cast<h8*>(planes + 3 * a.planeStride + off) = q1;
+  }
+}
+
+template <int G>
+__device__ __forceinline__ void splitWindowF16(const CfFirArgs& a, const CfWindow<G>& w, int8_t* planes, int tid,
+                                               float scale) {
+#pragma unroll
+  for (int j = 0; j < G; ++j) splitGroupF16<G>(a, w, planes, tid, scale, j);
+}
+
+struct CfF16State {
+  int sx;       // scale exponent of the tile
+  bool direct;  // that tile takes the direct path
+};
+
+// One tile of the double-buffered f16 kernel. On entry the planes of tile i are in set i & 1, wCur
+// holds tile i + 1's window and `nx` its statistics, wNext is free: it receives tile i + 2's loads
+// right away. The split of tile i + 1 runs between the MFMAs of tile i; tile i + 2's statistics
+// travel with tile i's partial sums through the same barrier. Two barriers per tile.
+template <int KS, int G, int EPI>
+__device__ __forceinline__ void cfF16Tile(const CfFirArgs& a, int8_t* smem, float* part, float (*red2)[2][kCfWaves],
+                                          const h8 (&bh)[kCfMaxKS], const h8 (&bl)[kCfMaxKS], int sh, int i, int n,
+                                          int t0, int tid, CfWindow<G>& wCur, CfWindow<G>& wNext, CfF16State& st,
+                                          CfF16State& nx) {
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int half = lane >> 5;
+  const int col = lane & 31;
+  const int tile = t0 + i;
+  int8_t* cur = smem + (i & 1) * 4 * a.planeStride;
+  int8_t* nxt = smem + ((i + 1) & 1) * 4 * a.planeStride;
+  if (i + 2 < n && !(GSDR_CF_EXPERIMENT & 4)) loadWindow<G>(a, tile + 2, tid, wNext);
+  const bool splitNext = i + 1 < n && !nx.direct && !(GSDR_CF_EXPERIMENT & 1);
+  const float scaleN = ldexpf(1.0f, nx.sx);
+  if (st.direct) {
+    directTile<EPI>(a, tile, tid);
+    if (splitNext) splitWindowF16<G>(a, wCur, nxt, tid, scaleN);
+  } else {
+    const int arow = lane & 15;
+    const int comp = (lane >> 4) & 1;
+    const int uRow = 4 * a.D * arow + half;
+    const int8_t* pI = cur + comp * a.planeStride;
+    v16f acc = v16f{};
+#pragma unroll
+    for (int s = 0; s < kCfMaxKS; ++s) {
+      if (s < KS) {
+        const int u = uRow + 2 * (wave * KS + s);
+        const int off = 16 * cfPhys(u, a.padShift);
+        const h8 x0 = *reinterpret_cast<const h8*>(pI + off);
+        const h8 x1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
+        if (GSDR_CF_EXPERIMENT & 2) {
+          acc[s] += (float)x0[0] + (float)x1[1];
+        } else {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+          if (s == (KS * (j + 1)) / (G + 1) && splitNext) splitGroupF16<G>(a, wCur, nxt, tid, scaleN, j);
+      }
+    }
+    if (GSDR_CF_EXPERIMENT & 8) {
+      if (acc[0] + acc[7] + acc[13] == 1.2345f) reinterpret_cast<float*>(a.out)[lane] = 0.0f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
+    }
+  }
+  // tile i + 2's statistics (its loads had the MFMA phase to land); red2 alternates by tile
+  if (i + 2 < n && !(GSDR_CF_EXPERIMENT & 16)) cfStatsLocal<G>(a, wNext, tid, red2[i & 1]);
+  __syncthreads();  // partials and statistics published; `cur` read and `nxt` written by all waves
+  CfF16State nn{0, true};
+  if (i + 2 < n) {
+    if (GSDR_CF_EXPERIMENT & 16) nn.direct = false;
+    else nn.direct = cfStatsFinish(red2[i & 1], &nn.sx);
+  }
+  if (!st.direct && !(GSDR_CF_EXPERIMENT & 8)) {
+    float yi = 0.0f, yq = 0.0f;
+#pragma unroll
+    for (int v = 0; v < kCfWaves; ++v) {
+      yi += part[(v * 16 + wave) * kWave + lane];
+      yq += part[(v * 16 + wave + 8) * kWave + lane];
+    }
+    const float outScale = ldexpf(1.0f, -(st.sx + sh));
+    const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * half;
+    const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
+    if (k < a.nOut) {
+      if (EPI == kEpiAm) {
+        reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq}) * outScale;
+      } else {
+        reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
+      }
+    }
+  }
+  __syncthreads();  // every wave has read `part` before the next tile rewrites it
+  st = nx;
+  nx = nn;
+}
+
+// DB: two plane sets and two register windows (cfF16Tile); else one of each, the split after the
+// tile's reduction.
+template <int KS, int G, int EPI, bool DB>
+__global__ __launch_bounds__(kCfThreads, 1) void firCfF16MfmaKernel(CfFirArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  constexpr int kSets = DB ? 2 : 1;
+  float* part = reinterpret_cast<float*>(smem + 4 * kSets * a.planeStride);
+  __shared__ float red[2][kCfWaves];
+  __shared__ float red2[2][2][kCfWaves];  // DB: statistics of tiles i + 2, alternating
+  __shared__ float waveMax[kCfWaves];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int D = a.D, T = a.T;
+
+  const int q = a.tiles / (int)gridDim.x, r = a.tiles % (int)gridDim.x;
+  const int t0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
+  const int n = q + ((int)blockIdx.x < r ? 1 : 0);
+  if (n <= 0) return;
+
+  CfWindow<G> winA, winB;
+  loadWindow<G>(a, t0, tid, winB);
+
+  // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), block max, two scaled f16 limbs ----------
+  const int off0 = 31 * D;
+  const int span = off0 + 128 * KS;
+  float hm = 0.0f;
+  for (int i = tid; i < span; i += kCfThreads) {
+    const int j = i - off0;
+    const float h = (j >= 0 && j < T) ? a.taps[j] : 0.0f;
+    part[i] = h;
+    hm = fmaxf(hm, fabsf(h));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) hm = fmaxf(hm, __shfl_xor(hm, o));
+  if (lane == 0) waveMax[wave] = hm;
+  __syncthreads();
+  float hMax = waveMax[0];
+#pragma unroll
+  for (int v = 1; v < kCfWaves; ++v) hMax = fmaxf(hMax, waveMax[v]);
+  const int sh = hMax > 0.0f ? 14 - ilogbf(hMax) : 0;
+  const int half = lane >> 5;
+  const int col = lane & 31;
+  h8 bh[kCfMaxKS], bl[kCfMaxKS];
+#pragma unroll
+  for (int s = 0; s < kCfMaxKS; ++s) {
+    if (s < KS) {
+      const int kap = 16 * (wave * KS + s) + 8 * half;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float hs = ldexpf(part[off0 + kap + e - col * D], sh);
+        const _Float16 hi = (_Float16)hs;
+        bh[s][e] = hi;
+        bl[s][e] = (_Float16)(hs - (float)hi);
+      }
+    } else {
+      bh[s] = h8{};
+      bl[s] = h8{};
+    }
+  }
+  __syncthreads();  // the tap staging area becomes the partial-sum area
+
+  // ---- prologue: tile t0 into plane set 0; tile t0 + 1's window and statistics ---------------
+  CfF16State st{0, true};
+  st.direct = cfTileStats<G>(a, winB, tid, red, &st.sx);
+  if (!st.direct) splitWindowF16<G>(a, winB, smem, tid, ldexpf(1.0f, st.sx));
+  if (n > 1) loadWindow<G>(a, t0 + 1, tid, winA);
+  __syncthreads();
+
+  if constexpr (DB) {
+    CfF16State nx{0, true};
+    if (n > 1) nx.direct = cfTileStats<G>(a, winA, tid, red, &nx.sx);
+    for (int i = 0; i < n; i += 2) {
+      cfF16Tile<KS, G, EPI>(a, smem, part, red2, bh, bl, sh, i, n, t0, tid, winA, winB, st, nx);
+      if (i + 1 < n)
+        cfF16Tile<KS, G, EPI>(a, smem, part, red2, bh, bl, sh, i + 1, n, t0, tid, winB, winA, st, nx);
+    }
+  } else {
+    CfWindow<G>& win = winA;
+    const int arow = lane & 15;
+    const int comp = (lane >> 4) & 1;
+    const int uRow = 4 * D * arow + half;
+    const int8_t* pI = smem + comp * a.planeStride;
+    for (int i = 0; i < n; ++i) {
+      const int tile = t0 + i;
+      if (st.direct) {
+        directTile<EPI>(a, tile, tid);
+      } else {
+        v16f acc = v16f{};
+#pragma unroll
+        for (int s = 0; s < kCfMaxKS; ++s) {
+          if (s < KS) {
+            const int u = uRow + 2 * (wave * KS + s);
+            const int off = 16 * cfPhys(u, a.padShift);
+            const h8 x0 = *reinterpret_cast<const h8*>(pI + off);
+            const h8 x1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
+      }
+      __syncthreads();  // partials complete; every wave is done reading the planes
+      if (!st.direct) {
+        float yi = 0.0f, yq = 0.0f;
+#pragma unroll
+        for (int v = 0; v < kCfWaves; ++v) {
+          yi += part[(v * 16 + wave) * kWave + lane];
+          yq += part[(v * 16 + wave + 8) * kWave + lane];
+        }
+        const float outScale = ldexpf(1.0f, -(st.sx + sh));
+        const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * half;
+        const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
+        if (k < a.nOut) {
+          if (EPI == kEpiAm) {
+            reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq}) * outScale;
+          } else {
+            reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
+          }
+        }
+      }
+      if (i + 1 < n) {
+        // the next tile's statistics (two barriers, which also fence this tile's partial reads),
+        // its planes, then the loads of the one after
+        st.direct = cfTileStats<G>(a, win, tid, red, &st.sx);
+        if (!st.direct) splitWindowF16<G>(a, win, smem, tid, ldexpf(1.0f, st.sx));
+        if (i + 2 < n) loadWindow<G>(a, tile + 2, tid, win);
+        __syncthreads();
+      }
+    }
+  }
+}
+
 // ---- int8 IQ input -------------------------------------------------------------------------
 
 struct I8DecArgs {
@@ -505,26 +851,50 @@ CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes) {
   return best;
 }
 
-template <int KS, int G, int EPI>
+// F16: 0 = bf16 x 3, 1 = f16 x 2 single plane set, 2 = f16 x 2 double-buffered
+template <int F16, int KS, int G, int EPI>
 hipError_t launchCfG(const CfFirArgs& a, size_t lds, int grid, hipStream_t stream) {
+  auto kernel = F16 == 2 ? &firCfF16MfmaKernel<KS, G, EPI, true>
+                         : (F16 == 1 ? &firCfF16MfmaKernel<KS, G, EPI, false> : &firCfMfmaKernel<KS, G, EPI>);
   static std::once_flag once;
   static hipError_t attrErr = hipSuccess;
-  std::call_once(once, [] {
-    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(&firCfMfmaKernel<KS, G, EPI>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kCfDynLdsMax);
+  std::call_once(once, [kernel] {
+    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kCfDynLdsMax);
   });
   if (attrErr != hipSuccess) return attrErr;
-  hipLaunchKernelGGL((firCfMfmaKernel<KS, G, EPI>), dim3(grid), dim3(kCfThreads), lds, stream, a);
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kCfThreads), lds, stream, a);
   return hipGetLastError();
 }
 
-template <int KS>
+template <int F16, int KS>
 hipError_t launchCfKS(const CfFirArgs& a, size_t lds, int grid, int epi, hipStream_t stream) {
   const int G = (a.Wu + kCfThreads - 1) / kCfThreads;
   switch (G) {
-    case 1: return epi == kEpiAm ? launchCfG<KS, 1, kEpiAm>(a, lds, grid, stream) : launchCfG<KS, 1, kEpiComplex>(a, lds, grid, stream);
-    case 2: return epi == kEpiAm ? launchCfG<KS, 2, kEpiAm>(a, lds, grid, stream) : launchCfG<KS, 2, kEpiComplex>(a, lds, grid, stream);
-    default: return epi == kEpiAm ? launchCfG<KS, 3, kEpiAm>(a, lds, grid, stream) : launchCfG<KS, 3, kEpiComplex>(a, lds, grid, stream);
+    case 1: return epi == kEpiAm ? launchCfG<F16, KS, 1, kEpiAm>(a, lds, grid, stream) : launchCfG<F16, KS, 1, kEpiComplex>(a, lds, grid, stream);
+    case 2: return epi == kEpiAm ? launchCfG<F16, KS, 2, kEpiAm>(a, lds, grid, stream) : launchCfG<F16, KS, 2, kEpiComplex>(a, lds, grid, stream);
+    // three window groups: two register windows would not fit beside the tap fragments
+    default: {
+      constexpr int F = F16 == 2 ? 1 : F16;
+      return epi == kEpiAm ? launchCfG<F, KS, 3, kEpiAm>(a, lds, grid, stream) : launchCfG<F, KS, 3, kEpiComplex>(a, lds, grid, stream);
+    }
+  }
+}
+
+template <int F16>
+hipError_t launchCfAny(const CfFirArgs& a, size_t lds, int grid, int epi, hipStream_t stream) {
+  switch (a.KS) {
+    case 1: return launchCfKS<F16, 1>(a, lds, grid, epi, stream);
+    case 2: return launchCfKS<F16, 2>(a, lds, grid, epi, stream);
+    case 3: return launchCfKS<F16, 3>(a, lds, grid, epi, stream);
+    case 4: return launchCfKS<F16, 4>(a, lds, grid, epi, stream);
+    case 5: return launchCfKS<F16, 5>(a, lds, grid, epi, stream);
+    case 6: return launchCfKS<F16, 6>(a, lds, grid, epi, stream);
+    case 7: return launchCfKS<F16, 7>(a, lds, grid, epi, stream);
+    case 8: return launchCfKS<F16, 8>(a, lds, grid, epi, stream);
+    case 9: return launchCfKS<F16, 9>(a, lds, grid, epi, stream);
+    case 10: return launchCfKS<F16, 10>(a, lds, grid, epi, stream);
+    default: return launchCfKS<F16, 11>(a, lds, grid, epi, stream);
   }
 }
 
@@ -576,35 +946,36 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
   a.tiles = (int32_t)tiles;
   a.Wu = 60 * a.D + 16 * a.KS;
+  // f16 x 2 with a per-tile scale by default; GSDR_POLICY_CF_BF16 selects the bf16 x 3 kernel
+  // f16 x 2, double-buffered when two plane sets fit; GSDR_POLICY_CF_BF16 selects bf16 x 3
+  const bool f16 = (kernelPolicy() & GSDR_POLICY_CF_BF16) == 0;
   static std::mutex mu;
-  static int cachedD = -1, cachedKS = -1;
+  static int cachedD = -1, cachedKS = -1, cachedMode = -1;
   static CfLayout cached{};
+  static int cachedPlanes = 0;
   {
     std::lock_guard<std::mutex> lock(mu);
-    if (cachedD != a.D || cachedKS != a.KS) {
-      cached = cfPlaneLayout(a.D, a.KS, a.Wu, 6);
+    const int mode = f16 ? 1 : 0;
+    if (cachedD != a.D || cachedKS != a.KS || cachedMode != mode) {
+      cachedPlanes = f16 ? 8 : 6;
+      cached = cfPlaneLayout(a.D, a.KS, a.Wu, cachedPlanes);
+      if (f16 && cached.planeStride == 0) {  // two sets do not fit: one set
+        cachedPlanes = 4;
+        cached = cfPlaneLayout(a.D, a.KS, a.Wu, cachedPlanes);
+      }
       cachedD = a.D;
       cachedKS = a.KS;
+      cachedMode = mode;
     }
     a.padShift = cached.padShift;
     a.planeStride = cached.planeStride;
   }
-  const size_t lds = 6 * (size_t)a.planeStride + kCfPartialBytes;
+  const int nPlanes = cachedPlanes;
+  const size_t lds = nPlanes * (size_t)a.planeStride + kCfPartialBytes;
   if (a.planeStride == 0 || lds > (size_t)kCfDynLdsMax) return hipErrorInvalidValue;
   const int grid = (int)(tiles < 256 ? tiles : 256);
-  switch (a.KS) {
-    case 1: return launchCfKS<1>(a, lds, grid, epi, stream);
-    case 2: return launchCfKS<2>(a, lds, grid, epi, stream);
-    case 3: return launchCfKS<3>(a, lds, grid, epi, stream);
-    case 4: return launchCfKS<4>(a, lds, grid, epi, stream);
-    case 5: return launchCfKS<5>(a, lds, grid, epi, stream);
-    case 6: return launchCfKS<6>(a, lds, grid, epi, stream);
-    case 7: return launchCfKS<7>(a, lds, grid, epi, stream);
-    case 8: return launchCfKS<8>(a, lds, grid, epi, stream);
-    case 9: return launchCfKS<9>(a, lds, grid, epi, stream);
-    case 10: return launchCfKS<10>(a, lds, grid, epi, stream);
-    default: return launchCfKS<11>(a, lds, grid, epi, stream);
-  }
+  if (!f16) return launchCfAny<0>(a, lds, grid, epi, stream);
+  return nPlanes == 8 ? launchCfAny<2>(a, lds, grid, epi, stream) : launchCfAny<1>(a, lds, grid, epi, stream);
 }
 
 bool firI8DecMfmaEligible(size_t tapCount, size_t decimation, const void* in) {

@@ -61,7 +61,8 @@ constexpr int kI8TileOut = 512;                                        // 16 row
 #ifndef GSDR_I8_EXPERIMENT
 #define GSDR_I8_EXPERIMENT 0  // attribution builds only: 1 = skip split, 2 = skip MFMA, 4 = skip epilogue,
                               // 8 = no DMA (compute on stale LDS), 16 = no stores, 32 = clock stamps,
-                              // 64 = hi limb only (half the MFMAs), 128 = one A fragment read per tile
+                              // 64 = hi limb only (half the MFMAs), 128 = one A fragment read per tile,
+                              // 256 = i8 MFMAs in place of the f16 ones (energy probe, wrong results)
 #endif
 constexpr int kI8TilesPerWave = GSDR_I8_TILES_PER_WAVE;
 constexpr int kI8ChunkTiles = kI8Waves * kI8TilesPerWave;              // 8 tiles per chunk
@@ -216,8 +217,19 @@ __device__ __forceinline__ void tileMfma(const int8_t* planes, const h8 (&bf)[S]
     for (int u = 0; u < 2; ++u) {
       const h8 av = (GSDR_I8_EXPERIMENT & 128) ? a0 + (_Float16)s
                                                : *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0 + s, 2 * u + half));
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][0], acc, 0, 0, 0);
-      if (!(GSDR_I8_EXPERIMENT & 64)) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][1], acc, 0, 0, 0);
+      if constexpr ((GSDR_I8_EXPERIMENT & 256) != 0) {  // energy probe: the same count of i8 MFMAs
+        typedef int v16i __attribute__((ext_vector_type(16)));
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        v16i ia = __builtin_bit_cast(v16i, acc);
+        ia = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(v4i, av), __builtin_bit_cast(v4i, bf[s][u][0]),
+                                                   ia, 0, 0, 0);
+        ia = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(v4i, av), __builtin_bit_cast(v4i, bf[s][u][1]),
+                                                   ia, 0, 0, 0);
+        acc = __builtin_bit_cast(v16f, ia);
+      } else {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][0], acc, 0, 0, 0);
+        if (!(GSDR_I8_EXPERIMENT & 64)) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][1], acc, 0, 0, 0);
+      }
     }
   }
 }

@@ -199,6 +199,7 @@ def synth_wideband_cf32(seed: int, f1: float, f2: float, first: int, n: int,
 
 
 POLICY_NO_MFMA = 1  # include/gsdr/gsdr_amd.h GSDR_POLICY_NO_MFMA
+POLICY_CF_BF16 = 2  # GSDR_POLICY_CF_BF16
 
 
 def set_kernel_policy(flags: int) -> int:

@@ -6,10 +6,15 @@
 #include <vector>
 #include <cstring>
 
+#include <cstdint>
 #define DECL(N)                                                                                    \
   namespace c##N {                                                                                 \
   hipError_t launchFirCfMfma(const float*, const float*, size_t, size_t, void*, size_t, int, hipStream_t); \
+  uint32_t kernelPolicy() { return POLICY_FOR_VARIANTS; }                                          \
   }
+#ifndef POLICY_FOR_VARIANTS
+#define POLICY_FOR_VARIANTS 0u
+#endif
 VARIANT_DECLS
 
 typedef hipError_t (*LaunchFn)(const float*, const float*, size_t, size_t, void*, size_t, int, hipStream_t);

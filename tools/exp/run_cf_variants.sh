@@ -9,8 +9,9 @@ nosplit|-DGSDR_CF_EXPERIMENT=1
 nomfma|-DGSDR_CF_EXPERIMENT=2
 noload|-DGSDR_CF_EXPERIMENT=4
 noreduce|-DGSDR_CF_EXPERIMENT=8
-mfma_only|-DGSDR_CF_EXPERIMENT=13
-split_only|-DGSDR_CF_EXPERIMENT=10"}
+nostats|-DGSDR_CF_EXPERIMENT=16
+mfma_only|-DGSDR_CF_EXPERIMENT=29
+no_mfma_no_split|-DGSDR_CF_EXPERIMENT=3"}
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
   decls=""; table=""; objs=""; i=0
