@@ -30,6 +30,7 @@
 // exact in f16, so the window becomes two f16 planes (I, Q) with one split pass of 3 VALU per
 // sample pair, and the taps are scaled by a block-uniform 2^sc and split into two f16 limbs as in
 // fir_i8_mfma.hip: 2 v_mfma_f32_32x32x16_f16 per K-step instead of 6 bf16 products.
+#include <algorithm>
 #include <mutex>
 
 #include "kcommon.h"
@@ -625,6 +626,398 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfF16MfmaKernel(CfFirArgs a)
   }
 }
 
+// ---- wave-specialised f16 x 2 kernel (default cf32 MFMA path) ----------------------------------
+//
+// The barrier-synchronous kernels above keep all eight waves in the same phase, so the matrix
+// cores idle while every wave splits, reduces or waits at a barrier (C3 attribution: MFMA alone
+// 0.32 ms of 0.97). Here one 768-thread block per CU runs two roles that meet only through
+// counters in LDS:
+//   * 8 consumer waves (2 per SIMD): the split-K MFMA loop of the kernels above (tap fragments
+//     resident in VGPRs), then their 32x32 partial accumulators into LDS;
+//   * 4 producer waves (1 per SIMD): window loads (two register windows, each group refilled with
+//     the tile two ahead right after it is split), the tile statistics, the split into one of two
+//     plane sets, and the reduction + epilogue of the previous tile's partials.
+// A producer's split of tile i + 1 and its reduction of tile i - 1 run on the vector ALUs while
+// the consumers' MFMAs of tile i run on the matrix cores of the same SIMDs.
+//
+// Hand-off counters (monotonic, one increment per wave): planesFull[set] (producers -> consumers:
+// tile's planes and mode written), planesFree[set] (consumers finished reading the set),
+// partsFull (consumer partials written), partsFree (producers read them), pstat (producer-local
+// statistics of the next tile published). Every wait is bounded: a wave that spins past the limit
+// raises `abort`, which releases every other wait, so the grid always drains.
+
+constexpr int kWsProducers = 4;
+constexpr int kWsPThreads = kWsProducers * kWave;           // 256
+constexpr int kWsThreads = kCfThreads + kWsPThreads;        // 768
+constexpr int kWsDirect = 0x7fffffff;                       // plane-set mode: direct fp32 tile
+constexpr int kWsSpinLimit = 1 << 22;                       // s_sleep(1) iterations (~0.1 s)
+
+struct WsCtl {
+  int planesFull[2];
+  int planesFree[2];
+  int partsFull;
+  int partsFree;
+  int pstat;
+  int tapsRead;                       // consumer waves done reading the taps staged in `part`
+  int abort;
+  int mode[2];                        // per plane set: scale exponent sx, or kWsDirect
+  float stat[2][2][kWsProducers];     // [tile parity][max, smallest block max][producer wave]
+};
+
+__device__ __forceinline__ void wsSignal(int* p, int lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS writes/reads complete
+  if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+#if GSDR_CF_EXPERIMENT & 32
+// attribution builds: per (block, wave) cycles spent in wsWait, and the wave's total cycles
+__device__ unsigned long long gWsStamp[256 * 12][2];
+#endif
+
+__device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
+#if GSDR_CF_EXPERIMENT & 32
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+  for (int it = 0;; ++it) {
+    const int v = waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (v >= target) break;
+    if (waveUniform(__hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
+    if (it > kWsSpinLimit) {
+      __hip_atomic_store(&c->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#if GSDR_CF_EXPERIMENT & 32
+  if ((threadIdx.x & 63) == 0)
+    gWsStamp[blockIdx.x * 12 + (threadIdx.x >> 6)][0] += __builtin_amdgcn_s_memtime() - t0;
+#endif
+}
+
+// Producer window: G units (8 samples, 64 B) per producer thread, unit g = ptid + 256 j; only the
+// Wl units that hold window samples are loaded (the K padding beyond them stays zero in LDS).
+// Buffer loads against a per-tile descriptor whose range ends at the input's last byte: past the
+// end they return zeros (finite; those samples meet zero taps or feed outputs >= nOut), so no
+// per-load clamping, one 32-bit offset per unit and the 64-bit base in SGPRs.
+// Loads are never skipped by a branch: the compiler's wait counting is exact only when every path
+// issues the same loads, so a window past the block's last tile gets an empty range (no traffic).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wsTileRsrc(const CfFirArgs& a, int tile, bool valid = true) {
+  const int64_t first = (int64_t)tile * kCfTileOut * a.D;  // first window sample
+  const int64_t left = valid ? a.nIn - first : 0;          // >= 1 for every tile
+  const int64_t bytes = left * 8 < 0x7fffffff ? left * 8 : 0x7fffffff;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x) + 2 * first, (short)0, (int)bytes, 0x00020000);
+}
+
+template <int G>
+__device__ __forceinline__ void wsLoadGroup(__amdgpu_buffer_rsrc_t rsrc, int Wl, int ptid, int j, CfWindow<G>& w) {
+  const int g = ptid + kWsPThreads * j;
+  const int voff = g < Wl ? 64 * g : 0x7ffffff0;  // unused unit: out of range, reads nothing
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    w.v[j][q] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16 * q, 0, 0));
+}
+
+// Branch-free (see wsTileRsrc): a unit past Wl holds zeros (its load was out of range) and is
+// written to the spare unit Wu that no A fragment reads.
+template <int G>
+__device__ __forceinline__ void wsSplitGroup(const CfFirArgs& a, int Wl, const CfWindow<G>& w, int8_t* planes,
+                                             int ptid, float scale, int j) {
+  const int g = ptid + kWsPThreads * j;
+  h8 i0, i1, q0, q1;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {  // samples 2q, 2q + 1: (re, im, re, im)
+    const f4 v = w.v[j][q] * scale;
+    const _Float16 a0 = (_Float16)v.x, b0 = (_Float16)v.y, c0 = (_Float16)v.z, d0 = (_Float16)v.w;
+    i0[2 * q] = a0;
+    i0[2 * q + 1] = c0;
+    q0[2 * q] = b0;
+    q0[2 * q + 1] = d0;
+    i1[2 * q] = (_Float16)(v.x - (float)a0);
+    i1[2 * q + 1] = (_Float16)(v.z - (float)c0);
+    q1[2 * q] = (_Float16)(v.y - (float)b0);
+    q1[2 * q + 1] = (_Float16)(v.w - (float)d0);
+  }
+  const int off = 16 * cfPhys(g < Wl ? g : a.Wu, a.padShift);
+  *reinterpret_cast<h8*>(planes + off) = i0;
+  *reinterpret_cast<h8*>(planes + a.planeStride + off) = q0;
+  *reinterpret_cast<h8*>(planes + 2 * a.planeStride + off) = i1;
+  *reinterpret_cast<h8*>(planes + 3 * a.planeStride + off) = q1;
+}
+
+// Producer-local statistics of a window (as cfStatsLocal over the producer threads).
+template <int G>
+__device__ __forceinline__ void wsStatsLocal(int Wl, const CfWindow<G>& w, int ptid, WsCtl* c, int parity) {
+  const int lane = ptid & (kWave - 1);
+  const int pw = ptid >> 6;
+  float m = 0.0f;
+  float bmin = INFINITY;
+  f4 probe = f4{};
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    float um = 0.0f;  // units past Wl read as zeros: no effect on either statistic
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f4 v = w.v[j][q];
+      probe += v * 0.0f;
+      um = fmaxf(um, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    float bm = um;  // 64-sample block = 8 consecutive units = 8 consecutive lanes
+    bm = fmaxf(bm, __shfl_xor(bm, 1));
+    bm = fmaxf(bm, __shfl_xor(bm, 2));
+    bm = fmaxf(bm, __shfl_xor(bm, 4));
+    m = fmaxf(m, um);
+    if (bm > 0.0f) bmin = fminf(bmin, bm);
+  }
+  const float pr = (probe.x + probe.y) + (probe.z + probe.w);
+  if (pr != pr) m = INFINITY;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    m = fmaxf(m, __shfl_xor(m, o));
+    bmin = fminf(bmin, __shfl_xor(bmin, o));
+  }
+  if (lane == 0) {
+    c->stat[parity][0][pw] = m;
+    c->stat[parity][1][pw] = bmin;
+  }
+}
+
+__device__ __forceinline__ bool wsStatsFinish(const WsCtl* c, int parity, int* sxOut) {
+  float M = c->stat[parity][0][0], B = c->stat[parity][1][0];
+#pragma unroll
+  for (int v = 1; v < kWsProducers; ++v) {
+    M = fmaxf(M, c->stat[parity][0][v]);
+    B = fminf(B, c->stat[parity][1][v]);
+  }
+  *sxOut = 0;
+  if (!(M <= 3.0e38f)) return true;
+  if (M == 0.0f) return false;
+  if (M < 1.0e-30f || B < M * (1.0f / 65536.0f)) return true;
+  *sxOut = 14 - ilogbf(M);
+  return false;
+}
+
+// Producer: reduce tile `tile`'s partials (8 consumer waves) and store its outputs.
+template <int EPI>
+__device__ __forceinline__ void wsReduce(const CfFirArgs& a, const float* part, int tile, int sx, int sh, int ptid) {
+  const int lane = ptid & (kWave - 1);
+  const float outScale = ldexpf(1.0f, -(sx + sh));
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int w = (ptid >> 6) + 4 * h;  // accumulator registers w (I) and w + 8 (Q)
+    float yi = 0.0f, yq = 0.0f;
+#pragma unroll
+    for (int v = 0; v < kCfWaves; ++v) {
+      yi += part[(v * 16 + w) * kWave + lane];
+      yq += part[(v * 16 + w + 8) * kWave + lane];
+    }
+    const int orow = (w & 3) + 8 * (w >> 2) + 4 * (lane >> 5);
+    const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + (lane & 31);
+    if (k < a.nOut) {
+      if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq}) * outScale;
+      else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
+    }
+  }
+}
+
+struct WsProdState {
+  int prevSx;
+  bool prevDirect;
+};
+
+// Producer, tile i: wCur holds tile i's window, wNext tile i + 1's (in flight).
+template <int G, int EPI>
+__device__ __forceinline__ void wsProducerTile(const CfFirArgs& a, int Wl, int8_t* smem, const float* part, WsCtl* c,
+                                               int sh, int t0, int n, int i, int ptid, CfWindow<G>& wCur,
+                                               CfWindow<G>& wNext, WsProdState& ps) {
+  const int lane = ptid & (kWave - 1);
+  const int set = i & 1;
+  const int tile = t0 + i;
+  wsWait(c, &c->pstat, kWsProducers * (i + 1));
+  int sx = 0;
+  const bool direct = wsStatsFinish(c, set, &sx);
+  wsWait(c, &c->planesFree[set], kCfWaves * (i >> 1));
+  int8_t* planes = smem + set * 4 * a.planeStride;
+  const float scale = ldexpf(1.0f, sx);
+  const __amdgpu_buffer_rsrc_t rsrc2 = wsTileRsrc(a, tile + 2, i + 2 < n && !(GSDR_CF_EXPERIMENT & 4));
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    if (!direct && !(GSDR_CF_EXPERIMENT & 1)) wsSplitGroup<G>(a, Wl, wCur, planes, ptid, scale, j);
+    wsLoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
+    asm volatile("" ::: "memory");  // one group's split temporaries live at a time
+  }
+  if (ptid == 0) c->mode[set] = direct ? kWsDirect : sx;
+  wsSignal(&c->planesFull[set], lane);
+  // unconditional (past the last tile: statistics of an empty window, never read), so that every
+  // path waits for wNext's loads at the same point and the loop-carried wait counts stay exact
+  wsStatsLocal<G>(Wl, wNext, ptid, c, (i + 1) & 1);
+  wsSignal(&c->pstat, lane);
+  if (i >= 1) {
+    wsWait(c, &c->partsFull, kCfWaves * i);
+    if (!ps.prevDirect && !(GSDR_CF_EXPERIMENT & 8)) wsReduce<EPI>(a, part, tile - 1, ps.prevSx, sh, ptid);
+    wsSignal(&c->partsFree, lane);
+  }
+  ps.prevSx = sx;
+  ps.prevDirect = direct;
+}
+
+template <int KS, int G, int EPI>
+__global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int Wl) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  float* part = reinterpret_cast<float*>(smem + 8 * a.planeStride);
+  __shared__ WsCtl ctl;
+  __shared__ float waveMax[kCfWaves + kWsProducers];
+  WsCtl* c = &ctl;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int D = a.D, T = a.T;
+
+  const int q = a.tiles / (int)gridDim.x, r = a.tiles % (int)gridDim.x;
+  const int t0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
+  const int n = q + ((int)blockIdx.x < r ? 1 : 0);
+  if (n <= 0) return;
+
+  const int ptid = tid - kCfThreads;
+#if GSDR_CF_EXPERIMENT & 32
+  const uint64_t tStart = __builtin_amdgcn_s_memtime();
+#define WS_STAMP_END() \
+  if (lane == 0) gWsStamp[blockIdx.x * 12 + wave][1] += __builtin_amdgcn_s_memtime() - tStart
+#else
+#define WS_STAMP_END() (void)0
+#endif
+
+  // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), block max; zero both plane sets --------
+  if (tid < (int)(sizeof(WsCtl) / 4)) reinterpret_cast<int*>(c)[tid] = 0;
+  const int off0 = 31 * D;
+  const int span = off0 + 128 * KS;
+  float hm = 0.0f;
+  for (int i = tid; i < span; i += kWsThreads) {
+    const int j = i - off0;
+    const float h = (j >= 0 && j < T) ? a.taps[j] : 0.0f;
+    part[i] = h;
+    hm = fmaxf(hm, fabsf(h));
+  }
+  for (int i = tid; i < 8 * a.planeStride / 16; i += kWsThreads) reinterpret_cast<uint4*>(smem)[i] = uint4{0, 0, 0, 0};
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) hm = fmaxf(hm, __shfl_xor(hm, o));
+  if (lane == 0) waveMax[wave] = hm;
+  __syncthreads();
+  float hMax = waveMax[0];
+#pragma unroll
+  for (int v = 1; v < kCfWaves + kWsProducers; ++v) hMax = fmaxf(hMax, waveMax[v]);
+  const int sh = hMax > 0.0f ? 14 - ilogbf(hMax) : 0;
+
+  if (wave >= kCfWaves) {
+    // ================= producers =================
+    CfWindow<G> wA, wB;
+    const __amdgpu_buffer_rsrc_t r0 = wsTileRsrc(a, t0);
+#pragma unroll
+    for (int j = 0; j < G; ++j) wsLoadGroup<G>(r0, Wl, ptid, j, wA);
+    const __amdgpu_buffer_rsrc_t r1 = wsTileRsrc(a, t0 + 1, n > 1);
+#pragma unroll
+    for (int j = 0; j < G; ++j) wsLoadGroup<G>(r1, Wl, ptid, j, wB);
+    wsStatsLocal<G>(Wl, wA, ptid, c, 0);
+    wsSignal(&c->pstat, lane);
+    WsProdState ps{0, true};
+    // the back-edge only after the second tile: a path that skipped it would leave wA's loads as
+    // the newest on entry and make the compiler's wait counts conservative for both windows
+    for (int i = 0;; i += 2) {
+      wsProducerTile<G, EPI>(a, Wl, smem, part, c, sh, t0, n, i, ptid, wA, wB, ps);
+      if (i + 1 >= n) break;
+      wsProducerTile<G, EPI>(a, Wl, smem, part, c, sh, t0, n, i + 1, ptid, wB, wA, ps);
+      if (i + 2 >= n) break;
+    }
+    wsWait(c, &c->partsFull, kCfWaves * n);
+    if (!ps.prevDirect) wsReduce<EPI>(a, part, t0 + n - 1, ps.prevSx, sh, ptid);
+    WS_STAMP_END();
+    return;
+  }
+
+  // ================= consumers =================
+  const int half = lane >> 5;
+  const int col = lane & 31;
+  h8 bh[kCfMaxKS], bl[kCfMaxKS];
+#pragma unroll
+  for (int s = 0; s < kCfMaxKS; ++s) {
+    if (s < KS) {
+      const int kap = 16 * (wave * KS + s) + 8 * half;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float hs = ldexpf(part[off0 + kap + e - col * D], sh);
+        const _Float16 hi = (_Float16)hs;
+        bh[s][e] = hi;
+        bl[s][e] = (_Float16)(hs - (float)hi);
+      }
+    } else {
+      bh[s] = h8{};
+      bl[s] = h8{};
+    }
+  }
+  // no barrier past this point (the roles diverge): the tap staging area becomes the partial-sum
+  // area once every consumer wave has its fragments (tapsRead, awaited before the first partials)
+  wsSignal(&c->tapsRead, lane);
+
+  const int arow = lane & 15;
+  const int comp = (lane >> 4) & 1;
+  const int uRow = 4 * D * arow + half;
+  for (int i = 0; i < n; ++i) {
+    const int set = i & 1;
+    const int tile = t0 + i;
+    wsWait(c, &c->planesFull[set], kWsProducers * ((i >> 1) + 1));
+    const int mode = waveUniform(c->mode[set]);
+    if (mode == kWsDirect) {
+      wsSignal(&c->planesFree[set], lane);
+      directTile<EPI>(a, tile, tid);
+      // keep partsFull in step with the producers' reductions: a wave may run at most one tile
+      // ahead of the partials the producers have consumed
+      wsWait(c, &c->partsFree, kWsProducers * i);
+      wsSignal(&c->partsFull, lane);
+      continue;
+    }
+    const int8_t* pI = smem + set * 4 * a.planeStride + comp * a.planeStride;
+    v16f acc = v16f{};
+    // A fragments one K-step ahead; the empty asm keeps the scheduler from hoisting more reads
+    // (168 VGPRs: the tap fragments already hold 88)
+    h8 x0, x1;
+    {
+      const int off = 16 * cfPhys(uRow + 2 * wave * KS, a.padShift);
+      x0 = *reinterpret_cast<const h8*>(pI + off);
+      x1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
+    }
+#pragma unroll
+    for (int s = 0; s < kCfMaxKS; ++s) {
+      if (s < KS) {
+        h8 n0 = x0, n1 = x1;
+        if (s + 1 < KS) {
+          const int off = 16 * cfPhys(uRow + 2 * (wave * KS + s + 1), a.padShift);
+          n0 = *reinterpret_cast<const h8*>(pI + off);
+          n1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
+        }
+        asm volatile("" ::: "memory");
+        if (GSDR_CF_EXPERIMENT & 2) {
+          acc[s] += (float)x0[0] + (float)x1[1];
+        } else {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
+        }
+        x0 = n0;
+        x1 = n1;
+      }
+    }
+    wsSignal(&c->planesFree[set], lane);  // this wave's A reads are complete
+    wsWait(c, &c->partsFree, kWsProducers * i);
+    if (i == 0) wsWait(c, &c->tapsRead, kCfWaves);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
+    wsSignal(&c->partsFull, lane);
+  }
+  WS_STAMP_END();
+}
+#undef WS_STAMP_END
+
 // ---- int8 IQ input -------------------------------------------------------------------------
 
 struct I8DecArgs {
@@ -912,6 +1305,46 @@ hipError_t launchI8DecG(const I8DecArgs& a, size_t lds, int grid, hipStream_t st
   return hipGetLastError();
 }
 
+template <int KS, int G, int EPI>
+hipError_t launchCfWsG(const CfFirArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
+  auto kernel = &firCfWsKernel<KS, G, EPI>;
+  static std::once_flag once;
+  static hipError_t attrErr = hipSuccess;
+  std::call_once(once, [kernel] {
+    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kCfDynLdsMax);
+  });
+  if (attrErr != hipSuccess) return attrErr;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWsThreads), lds, stream, a, Wl);
+  return hipGetLastError();
+}
+
+template <int KS>
+hipError_t launchCfWsKS(const CfFirArgs& a, int Wl, size_t lds, int grid, int epi, hipStream_t stream) {
+  const int G = (Wl + kWsPThreads - 1) / kWsPThreads;
+  switch (G) {
+    case 1: return epi == kEpiAm ? launchCfWsG<KS, 1, kEpiAm>(a, Wl, lds, grid, stream) : launchCfWsG<KS, 1, kEpiComplex>(a, Wl, lds, grid, stream);
+    case 2: return epi == kEpiAm ? launchCfWsG<KS, 2, kEpiAm>(a, Wl, lds, grid, stream) : launchCfWsG<KS, 2, kEpiComplex>(a, Wl, lds, grid, stream);
+    default: return epi == kEpiAm ? launchCfWsG<KS, 3, kEpiAm>(a, Wl, lds, grid, stream) : launchCfWsG<KS, 3, kEpiComplex>(a, Wl, lds, grid, stream);
+  }
+}
+
+hipError_t launchCfWsAny(const CfFirArgs& a, int Wl, size_t lds, int grid, int epi, hipStream_t stream) {
+  switch (a.KS) {
+    case 1: return launchCfWsKS<1>(a, Wl, lds, grid, epi, stream);
+    case 2: return launchCfWsKS<2>(a, Wl, lds, grid, epi, stream);
+    case 3: return launchCfWsKS<3>(a, Wl, lds, grid, epi, stream);
+    case 4: return launchCfWsKS<4>(a, Wl, lds, grid, epi, stream);
+    case 5: return launchCfWsKS<5>(a, Wl, lds, grid, epi, stream);
+    case 6: return launchCfWsKS<6>(a, Wl, lds, grid, epi, stream);
+    case 7: return launchCfWsKS<7>(a, Wl, lds, grid, epi, stream);
+    case 8: return launchCfWsKS<8>(a, Wl, lds, grid, epi, stream);
+    case 9: return launchCfWsKS<9>(a, Wl, lds, grid, epi, stream);
+    case 10: return launchCfWsKS<10>(a, Wl, lds, grid, epi, stream);
+    default: return launchCfWsKS<11>(a, Wl, lds, grid, epi, stream);
+  }
+}
+
 template <int KS>
 hipError_t launchI8DecKS(const I8DecArgs& a, size_t lds, int grid, int epi, hipStream_t stream) {
   const int G = (a.Wu + kCfThreads - 1) / kCfThreads;
@@ -923,6 +1356,19 @@ hipError_t launchI8DecKS(const I8DecArgs& a, size_t lds, int grid, int epi, hipS
 }
 
 }  // namespace
+
+// Attribution builds (tools/exp/cf_bench): copy out and clear the wave-specialised kernel's stamps.
+hipError_t wsReadStamps(unsigned long long* host) {
+#if GSDR_CF_EXPERIMENT & 32
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(gWsStamp), sizeof(gWsStamp));
+  static unsigned long long zeros[256 * 12][2];
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(gWsStamp), zeros, sizeof(gWsStamp));
+  return e;
+#else
+  (void)host;
+  return hipErrorNotSupported;
+#endif
+}
 
 bool firCfMfmaEligible(size_t tapCount, size_t decimation, const void* in) {
   const size_t d = decimation < 1 ? 1 : decimation;
@@ -946,9 +1392,38 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
   a.tiles = (int32_t)tiles;
   a.Wu = 60 * a.D + 16 * a.KS;
-  // f16 x 2 with a per-tile scale by default; GSDR_POLICY_CF_BF16 selects the bf16 x 3 kernel
-  // f16 x 2, double-buffered when two plane sets fit; GSDR_POLICY_CF_BF16 selects bf16 x 3
-  const bool f16 = (kernelPolicy() & GSDR_POLICY_CF_BF16) == 0;
+  // f16 x 2 with a per-tile scale by default: the wave-specialised kernel when two plane sets fit
+  // and a producer thread holds at most 3 window units, else the barrier-synchronous one (double-
+  // buffered when two plane sets fit); GSDR_POLICY_CF_BF16 selects bf16 x 3
+#ifdef GSDR_FORCE_POLICY  // variant builds only (tools/exp)
+  const uint32_t policy = GSDR_FORCE_POLICY;
+#else
+  const uint32_t policy = kernelPolicy();
+#endif
+  const bool f16 = (policy & GSDR_POLICY_CF_BF16) == 0;
+  const int grid = (int)(tiles < 256 ? tiles : 256);
+  const int Wl = std::min(a.Wu, (511 * a.D + a.T + 7) / 8);  // units holding window samples
+  if (f16 && (policy & GSDR_POLICY_NO_WS) == 0 && Wl <= 3 * kWsPThreads) {
+    static std::mutex wsMu;
+    static int wsD = -1, wsKS = -1;
+    static CfLayout wsLayout{};
+    CfLayout lay;
+    {
+      std::lock_guard<std::mutex> lock(wsMu);
+      if (wsD != a.D || wsKS != a.KS) {
+        wsLayout = cfPlaneLayout(a.D, a.KS, a.Wu, 8);
+        wsD = a.D;
+        wsKS = a.KS;
+      }
+      lay = wsLayout;
+    }
+    if (lay.planeStride != 0) {
+      a.padShift = lay.padShift;
+      a.planeStride = lay.planeStride;
+      const size_t lds = 8 * (size_t)a.planeStride + kCfPartialBytes;
+      if (lds <= (size_t)kCfDynLdsMax) return launchCfWsAny(a, Wl, lds, grid, epi, stream);
+    }
+  }
   static std::mutex mu;
   static int cachedD = -1, cachedKS = -1, cachedMode = -1;
   static CfLayout cached{};
@@ -973,7 +1448,6 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
   const int nPlanes = cachedPlanes;
   const size_t lds = nPlanes * (size_t)a.planeStride + kCfPartialBytes;
   if (a.planeStride == 0 || lds > (size_t)kCfDynLdsMax) return hipErrorInvalidValue;
-  const int grid = (int)(tiles < 256 ? tiles : 256);
   if (!f16) return launchCfAny<0>(a, lds, grid, epi, stream);
   return nPlanes == 8 ? launchCfAny<2>(a, lds, grid, epi, stream) : launchCfAny<1>(a, lds, grid, epi, stream);
 }

@@ -200,6 +200,7 @@ def synth_wideband_cf32(seed: int, f1: float, f2: float, first: int, n: int,
 
 POLICY_NO_MFMA = 1  # include/gsdr/gsdr_amd.h GSDR_POLICY_NO_MFMA
 POLICY_CF_BF16 = 2  # GSDR_POLICY_CF_BF16
+POLICY_NO_WS = 4  # GSDR_POLICY_NO_WS: barrier-synchronous decimating MFMA kernels
 
 
 def set_kernel_policy(flags: int) -> int:

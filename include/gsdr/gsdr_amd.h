@@ -90,6 +90,9 @@ GSDR_API hipError_t gsdrInt8MixFirFCAmDemod(size_t decimation, const float* taps
 #define GSDR_POLICY_NO_MFMA 1u
 /* cf32 x real taps on the bf16 x 3 split (6 products) instead of f16 x 2 with per-tile scale. */
 #define GSDR_POLICY_CF_BF16 2u
+/* Decimating MFMA FIRs on the barrier-synchronous kernels instead of the wave-specialised
+ * (producer / consumer) ones. */
+#define GSDR_POLICY_NO_WS 4u
 GSDR_API void gsdrAmdSetKernelPolicy(uint32_t flags);
 GSDR_API uint32_t gsdrAmdGetKernelPolicy(void);
 

@@ -309,6 +309,36 @@ def test_cf_mfma_dynamic_range(ops, orc):
     _check_fir(y, y64, bound, "dynamic-range")
 
 
+@pytest.mark.parametrize("T,D,n_out,quiet", [(1023, 10, 300_000, True), (1023, 1, 200_000, False),
+                                             (255, 4, 150_001, True), (64, 2, 70_000, False)])
+def test_cf_mfma_wave_specialised_matches_sync(ops, orc, T, D, n_out, quiet):
+    """The wave-specialised (producer / consumer) cf32 MFMA kernel performs the same arithmetic in
+    the same order as the barrier-synchronous one, also across direct-path tiles (quiet
+    stretches) and with several tiles per block; and stays within tolerance of float64."""
+    rng = np.random.default_rng(T + 7 * D)
+    n_in = (n_out - 1) * D + T
+    x = (rng.standard_normal(n_in) + 1j * rng.standard_normal(n_in)).astype(np.complex64)
+    if quiet:
+        x[(np.arange(n_in) // 20_000) % 5 == 3] *= np.float32(1e-7)
+    taps = orc.lowpass_taps(T, 0.4 / D).astype(np.float32)
+    x_d, taps_d = _dev(x), _dev(taps)
+    for am in (False, True):
+        y_ws = _host(ops.fir(taps_d, x_d, D, n_out, am=am))
+        prev = ops.set_kernel_policy(ops.POLICY_NO_WS)
+        try:
+            y_sync = _host(ops.fir(taps_d, x_d, D, n_out, am=am))
+        finally:
+            ops.set_kernel_policy(prev)
+        # identical arithmetic; only the K-padding units that the synchronous kernel also folds
+        # into a tile's scale statistics may move a tile's scale (or direct decision)
+        diff = y_ws != y_sync
+        assert diff.mean() <= 0.01, ("ws-vs-sync", T, D, n_out, am, int(diff.sum()))
+        assert np.max(np.abs(y_ws - y_sync)) <= 1e-6 * np.max(np.abs(y_sync)), ("ws-vs-sync", T, D, am)
+    sl = slice(0, min(n_out, 20_000))
+    y64, bound = orc.fir_f64(taps, x[: (sl.stop - 1) * D + T], D, sl.stop)
+    _check_fir(_host(ops.fir(taps_d, x_d, D, n_out))[sl], y64, bound, ("ws", T, D))
+
+
 def test_cf_mfma_misaligned_falls_back(ops, orc):
     T, D, n_out = 255, 4, 3000
     rng = np.random.default_rng(9)

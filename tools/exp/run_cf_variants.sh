@@ -19,7 +19,7 @@ if [ "${1:-build}" = build ]; then
     [ -z "$name" ] && continue
     hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Iinclude -Icuda-sdr_amd/csrc/kernels -mllvm -amdgpu-mfma-vgpr-form \
       -Dgsdr_amd=c$i $flags -c $KSRC -o $OUT/c$i.o &
-    decls="$decls DECL($i)"; table="$table {\"$name\", c$i::launchFirCfMfma},"; objs="$objs $OUT/c$i.o"
+    decls="$decls DECL($i)"; table="$table {\"$name\", c$i::launchFirCfMfma, c$i::wsReadStamps},"; objs="$objs $OUT/c$i.o"
     i=$((i+1))
   done <<< "$VARIANTS"
   wait
