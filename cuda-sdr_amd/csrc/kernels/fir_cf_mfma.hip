@@ -633,17 +633,18 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfF16MfmaKernel(CfFirArgs a)
 // 0.32 ms of 0.97). Here one 768-thread block per CU runs two roles that meet only through
 // counters in LDS:
 //   * 8 consumer waves (2 per SIMD): the split-K MFMA loop of the kernels above (tap fragments
-//     resident in VGPRs), then their 32x32 partial accumulators into LDS;
+//     resident in VGPRs), their 32x32 partial accumulators into LDS, and the reduction + epilogue
+//     of 64 outputs each (the synchronous kernels' epilogue, same summation order);
 //   * 4 producer waves (1 per SIMD): window loads (two register windows, each group refilled with
-//     the tile two ahead right after it is split), the tile statistics, the split into one of two
-//     plane sets, and the reduction + epilogue of the previous tile's partials.
-// A producer's split of tile i + 1 and its reduction of tile i - 1 run on the vector ALUs while
-// the consumers' MFMAs of tile i run on the matrix cores of the same SIMDs.
+//     the tile two ahead right after it is split), the tile statistics (DPP reductions, no LDS
+//     round trips) and the split into one of two plane sets.
+// A producer's split of tile i + 1 runs on the vector ALUs while the consumers' MFMAs of tile i
+// run on the matrix cores of the same SIMDs.
 //
 // Hand-off counters (monotonic, one increment per wave): planesFull[set] (producers -> consumers:
 // tile's planes and mode written), planesFree[set] (consumers finished reading the set),
-// partsFull (consumer partials written), partsFree (producers read them), pstat (producer-local
-// statistics of the next tile published). Every wait is bounded: a wave that spins past the limit
+// partsFull / partsFree (consumers among themselves: all partials of a tile written / all read),
+// pstat (producer-local statistics of the next tile published). Every wait is bounded: a wave that spins past the limit
 // raises `abort`, which releases every other wait, so the grid always drains.
 
 constexpr int kWsProducers = 4;
@@ -700,22 +701,46 @@ __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
 // Buffer loads against a per-tile descriptor whose range ends at the input's last byte: past the
 // end they return zeros (finite; those samples meet zero taps or feed outputs >= nOut), so no
 // per-load clamping, one 32-bit offset per unit and the 64-bit base in SGPRs.
-// Loads are never skipped by a branch: the compiler's wait counting is exact only when every path
-// issues the same loads, so a window past the block's last tile gets an empty range (no traffic).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wsTileRsrc(const CfFirArgs& a, int tile, bool valid = true) {
+// The loads are inline asm with explicit vmcnt waits: the producer issues no other vector memory
+// operations, every tile issues exactly 4 G loads (a window past the block's last tile gets an
+// empty range, no traffic), and the only wait - before a window's statistics - is vmcnt(4 G): the
+// window in question is then complete while the 4 G loads issued after it stay in flight. (The
+// compiler's own counting merged both register windows at the loop header and waited for the
+// newer window's loads before every split.)
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i4v wsTileRsrc(const CfFirArgs& a, int tile, bool valid = true) {
   const int64_t first = (int64_t)tile * kCfTileOut * a.D;  // first window sample
   const int64_t left = valid ? a.nIn - first : 0;          // >= 1 for every tile
   const int64_t bytes = left * 8 < 0x7fffffff ? left * 8 : 0x7fffffff;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x) + 2 * first, (short)0, (int)bytes, 0x00020000);
+  const uint64_t base = reinterpret_cast<uint64_t>(a.x + 2 * first);
+  i4v r;
+  r.x = waveUniform((int)(uint32_t)base);
+  r.y = waveUniform((int)((base >> 32) & 0xffffu));  // stride 0
+  r.z = waveUniform((int)bytes);                      // num_records (bytes)
+  r.w = 0x00020000;                                   // gfx9 raw buffer: dword3
+  return r;
 }
 
 template <int G>
-__device__ __forceinline__ void wsLoadGroup(__amdgpu_buffer_rsrc_t rsrc, int Wl, int ptid, int j, CfWindow<G>& w) {
+__device__ __forceinline__ void wsLoadGroup(i4v rsrc, int Wl, int ptid, int j, CfWindow<G>& w) {
   const int g = ptid + kWsPThreads * j;
   const int voff = g < Wl ? 64 * g : 0x7ffffff0;  // unused unit: out of range, reads nothing
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(w.v[j][0]) : "v"(voff), "s"(rsrc) : "memory");
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:16" : "=v"(w.v[j][1]) : "v"(voff), "s"(rsrc) : "memory");
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:32" : "=v"(w.v[j][2]) : "v"(voff), "s"(rsrc) : "memory");
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:48" : "=v"(w.v[j][3]) : "v"(voff), "s"(rsrc) : "memory");
+}
+
+// Wait until at most N of this wave's loads are outstanding, then pin the window's registers
+// behind the wait (the empty asm statements keep every use of them after it).
+template <int N, int G>
+__device__ __forceinline__ void wsWaitWindow(CfWindow<G>& w) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    w.v[j][q] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16 * q, 0, 0));
+  for (int j = 0; j < G; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(w.v[j][q]));
 }
 
 // Branch-free (see wsTileRsrc): a unit past Wl holds zeros (its load was out of range) and is
@@ -762,20 +787,14 @@ __device__ __forceinline__ void wsStatsLocal(int Wl, const CfWindow<G>& w, int p
       probe += v * 0.0f;
       um = fmaxf(um, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
-    float bm = um;  // 64-sample block = 8 consecutive units = 8 consecutive lanes
-    bm = fmaxf(bm, __shfl_xor(bm, 1));
-    bm = fmaxf(bm, __shfl_xor(bm, 2));
-    bm = fmaxf(bm, __shfl_xor(bm, 4));
+    const float bm = dppMax8(um);  // 64-sample block = 8 consecutive units = 8 consecutive lanes
     m = fmaxf(m, um);
     if (bm > 0.0f) bmin = fminf(bmin, bm);
   }
   const float pr = (probe.x + probe.y) + (probe.z + probe.w);
   if (pr != pr) m = INFINITY;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    m = fmaxf(m, __shfl_xor(m, o));
-    bmin = fminf(bmin, __shfl_xor(bmin, o));
-  }
+  m = waveMaxNonNeg(m);
+  bmin = waveMinNonNeg(bmin);
   if (lane == 0) {
     c->stat[parity][0][pw] = m;
     c->stat[parity][1][pw] = bmin;
@@ -797,68 +816,31 @@ __device__ __forceinline__ bool wsStatsFinish(const WsCtl* c, int parity, int* s
   return false;
 }
 
-// Producer: reduce tile `tile`'s partials (8 consumer waves) and store its outputs.
-template <int EPI>
-__device__ __forceinline__ void wsReduce(const CfFirArgs& a, const float* part, int tile, int sx, int sh, int ptid) {
-  const int lane = ptid & (kWave - 1);
-  const float outScale = ldexpf(1.0f, -(sx + sh));
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int w = (ptid >> 6) + 4 * h;  // accumulator registers w (I) and w + 8 (Q)
-    float yi = 0.0f, yq = 0.0f;
-#pragma unroll
-    for (int v = 0; v < kCfWaves; ++v) {
-      yi += part[(v * 16 + w) * kWave + lane];
-      yq += part[(v * 16 + w + 8) * kWave + lane];
-    }
-    const int orow = (w & 3) + 8 * (w >> 2) + 4 * (lane >> 5);
-    const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + (lane & 31);
-    if (k < a.nOut) {
-      if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq}) * outScale;
-      else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
-    }
-  }
-}
-
-struct WsProdState {
-  int prevSx;
-  bool prevDirect;
-};
-
 // Producer, tile i: wCur holds tile i's window, wNext tile i + 1's (in flight).
-template <int G, int EPI>
-__device__ __forceinline__ void wsProducerTile(const CfFirArgs& a, int Wl, int8_t* smem, const float* part, WsCtl* c,
-                                               int sh, int t0, int n, int i, int ptid, CfWindow<G>& wCur,
-                                               CfWindow<G>& wNext, WsProdState& ps) {
+template <int G>
+__device__ __forceinline__ void wsProducerTile(const CfFirArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
+                                               int i, int ptid, CfWindow<G>& wCur, CfWindow<G>& wNext) {
   const int lane = ptid & (kWave - 1);
   const int set = i & 1;
-  const int tile = t0 + i;
   wsWait(c, &c->pstat, kWsProducers * (i + 1));
   int sx = 0;
   const bool direct = wsStatsFinish(c, set, &sx);
   wsWait(c, &c->planesFree[set], kCfWaves * (i >> 1));
   int8_t* planes = smem + set * 4 * a.planeStride;
   const float scale = ldexpf(1.0f, sx);
-  const __amdgpu_buffer_rsrc_t rsrc2 = wsTileRsrc(a, tile + 2, i + 2 < n && !(GSDR_CF_EXPERIMENT & 4));
+  const i4v rsrc2 = wsTileRsrc(a, tile + 2, i + 2 < n && !(GSDR_CF_EXPERIMENT & 4));
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     if (!direct && !(GSDR_CF_EXPERIMENT & 1)) wsSplitGroup<G>(a, Wl, wCur, planes, ptid, scale, j);
     wsLoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
-    asm volatile("" ::: "memory");  // one group's split temporaries live at a time
   }
   if (ptid == 0) c->mode[set] = direct ? kWsDirect : sx;
   wsSignal(&c->planesFull[set], lane);
   // unconditional (past the last tile: statistics of an empty window, never read), so that every
   // path waits for wNext's loads at the same point and the loop-carried wait counts stay exact
+  wsWaitWindow<4 * G>(wNext);
   wsStatsLocal<G>(Wl, wNext, ptid, c, (i + 1) & 1);
   wsSignal(&c->pstat, lane);
-  if (i >= 1) {
-    wsWait(c, &c->partsFull, kCfWaves * i);
-    if (!ps.prevDirect && !(GSDR_CF_EXPERIMENT & 8)) wsReduce<EPI>(a, part, tile - 1, ps.prevSx, sh, ptid);
-    wsSignal(&c->partsFree, lane);
-  }
-  ps.prevSx = sx;
-  ps.prevDirect = direct;
 }
 
 template <int KS, int G, int EPI>
@@ -912,25 +894,24 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
   if (wave >= kCfWaves) {
     // ================= producers =================
     CfWindow<G> wA, wB;
-    const __amdgpu_buffer_rsrc_t r0 = wsTileRsrc(a, t0);
+    const i4v r0 = wsTileRsrc(a, t0);
 #pragma unroll
     for (int j = 0; j < G; ++j) wsLoadGroup<G>(r0, Wl, ptid, j, wA);
-    const __amdgpu_buffer_rsrc_t r1 = wsTileRsrc(a, t0 + 1, n > 1);
+    const i4v r1 = wsTileRsrc(a, t0 + 1, n > 1);
 #pragma unroll
     for (int j = 0; j < G; ++j) wsLoadGroup<G>(r1, Wl, ptid, j, wB);
+    wsWaitWindow<4 * G>(wA);
     wsStatsLocal<G>(Wl, wA, ptid, c, 0);
     wsSignal(&c->pstat, lane);
-    WsProdState ps{0, true};
     // the back-edge only after the second tile: a path that skipped it would leave wA's loads as
     // the newest on entry and make the compiler's wait counts conservative for both windows
     for (int i = 0;; i += 2) {
-      wsProducerTile<G, EPI>(a, Wl, smem, part, c, sh, t0, n, i, ptid, wA, wB, ps);
+      wsProducerTile<G>(a, Wl, smem, c, n, t0 + i, i, ptid, wA, wB);
       if (i + 1 >= n) break;
-      wsProducerTile<G, EPI>(a, Wl, smem, part, c, sh, t0, n, i + 1, ptid, wB, wA, ps);
+      wsProducerTile<G>(a, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, wA);
       if (i + 2 >= n) break;
     }
-    wsWait(c, &c->partsFull, kCfWaves * n);
-    if (!ps.prevDirect) wsReduce<EPI>(a, part, t0 + n - 1, ps.prevSx, sh, ptid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the wave
     WS_STAMP_END();
     return;
   }
@@ -970,10 +951,12 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
     if (mode == kWsDirect) {
       wsSignal(&c->planesFree[set], lane);
       directTile<EPI>(a, tile, tid);
-      // keep partsFull in step with the producers' reductions: a wave may run at most one tile
-      // ahead of the partials the producers have consumed
-      wsWait(c, &c->partsFree, kWsProducers * i);
+      // the partial hand-off counters advance as for any tile (they keep the waves within a tile
+      // of each other, which the count-based waits rely on)
+      wsWait(c, &c->partsFree, kCfWaves * i);
       wsSignal(&c->partsFull, lane);
+      wsWait(c, &c->partsFull, kCfWaves * (i + 1));
+      wsSignal(&c->partsFree, lane);
       continue;
     }
     const int8_t* pI = smem + set * 4 * a.planeStride + comp * a.planeStride;
@@ -1008,11 +991,31 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
       }
     }
     wsSignal(&c->planesFree[set], lane);  // this wave's A reads are complete
-    wsWait(c, &c->partsFree, kWsProducers * i);
+    wsWait(c, &c->partsFree, kCfWaves * i);  // every wave has read tile i - 1's partials
     if (i == 0) wsWait(c, &c->tapsRead, kCfWaves);
 #pragma unroll
     for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
     wsSignal(&c->partsFull, lane);
+    wsWait(c, &c->partsFull, kCfWaves * (i + 1));
+    if (!(GSDR_CF_EXPERIMENT & 8)) {
+      // wave w finishes accumulator register w (I) / w + 8 (Q), as the synchronous kernels
+      float yi = 0.0f, yq = 0.0f;
+#pragma unroll
+      for (int v = 0; v < kCfWaves; ++v) {
+        yi += part[(v * 16 + wave) * kWave + lane];
+        yq += part[(v * 16 + wave + 8) * kWave + lane];
+      }
+      wsSignal(&c->partsFree, lane);
+      const float outScale = ldexpf(1.0f, -(mode + sh));
+      const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * half;
+      const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
+      if (k < a.nOut) {
+        if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq}) * outScale;
+        else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
+      }
+    } else {
+      wsSignal(&c->partsFree, lane);
+    }
   }
   WS_STAMP_END();
 }

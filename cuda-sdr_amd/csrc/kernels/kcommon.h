@@ -32,6 +32,47 @@ __device__ __forceinline__ uint32_t xcdTile(uint32_t b, uint32_t nb) {
 
 __device__ __forceinline__ int waveUniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Cross-lane reductions on DPP (VALU) instead of ds_bpermute: no LDS round trip, which matters in
+// waves whose LDS queue is shared with MFMA operand reads. dpp_ctrl encodings (gfx9):
+// quad_perm [1,0,3,2] = 0xB1, [2,3,0,1] = 0x4E, row_mirror = 0x140, row_half_mirror = 0x141.
+template <int CTRL>
+__device__ __forceinline__ float dppF(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+// max over each aligned group of 8 lanes (the result in every lane of the group)
+__device__ __forceinline__ float dppMax8(float v) {
+  v = fmaxf(v, dppF<0x141>(v));
+  v = fmaxf(v, dppF<0xB1>(v));
+  return fmaxf(v, dppF<0x4E>(v));
+}
+__device__ __forceinline__ float dppMin8(float v) {
+  v = fminf(v, dppF<0x141>(v));
+  v = fminf(v, dppF<0xB1>(v));
+  return fminf(v, dppF<0x4E>(v));
+}
+// wave-wide max / min of NON-NEGATIVE floats (+inf allowed, no NaN): 8-lane groups by DPP, the
+// rows' halves by row_mirror, the four rows through SGPRs (bit patterns order like the values)
+__device__ __forceinline__ float waveMaxNonNeg(float v) {
+  v = dppMax8(v);
+  v = fmaxf(v, dppF<0x140>(v));
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  uint32_t m = __builtin_amdgcn_readlane(u, 0);
+  m = max(m, (uint32_t)__builtin_amdgcn_readlane(u, 16));
+  m = max(m, (uint32_t)__builtin_amdgcn_readlane(u, 32));
+  m = max(m, (uint32_t)__builtin_amdgcn_readlane(u, 48));
+  return __builtin_bit_cast(float, m);
+}
+__device__ __forceinline__ float waveMinNonNeg(float v) {
+  v = dppMin8(v);
+  v = fminf(v, dppF<0x140>(v));
+  const uint32_t u = __builtin_bit_cast(uint32_t, v);
+  uint32_t m = __builtin_amdgcn_readlane(u, 0);
+  m = min(m, (uint32_t)__builtin_amdgcn_readlane(u, 16));
+  m = min(m, (uint32_t)__builtin_amdgcn_readlane(u, 32));
+  m = min(m, (uint32_t)__builtin_amdgcn_readlane(u, 48));
+  return __builtin_bit_cast(float, m);
+}
+
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
 // Four interleaved int8 IQ words (I0 Q0 I1 Q1 each) -> the clamped samples x' = max(x, -127) of
