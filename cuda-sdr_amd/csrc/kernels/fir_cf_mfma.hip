@@ -672,7 +672,7 @@ __device__ __forceinline__ void wsSignal(int* p, int lane) {
 
 #if GSDR_CF_EXPERIMENT & 32
 // attribution builds: per (block, wave) cycles spent in wsWait, and the wave's total cycles
-__device__ unsigned long long gWsStamp[256 * 12][2];
+__device__ unsigned long long gWsStamp[256 * 16][2];
 #endif
 
 __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
@@ -692,7 +692,7 @@ __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 #if GSDR_CF_EXPERIMENT & 32
   if ((threadIdx.x & 63) == 0)
-    gWsStamp[blockIdx.x * 12 + (threadIdx.x >> 6)][0] += __builtin_amdgcn_s_memtime() - t0;
+    gWsStamp[blockIdx.x * 16 + (threadIdx.x >> 6)][0] += __builtin_amdgcn_s_memtime() - t0;
 #endif
 }
 
@@ -749,25 +749,30 @@ template <int G>
 __device__ __forceinline__ void wsSplitGroup(const CfFirArgs& a, int Wl, const CfWindow<G>& w, int8_t* planes,
                                              int ptid, float scale, int j) {
   const int g = ptid + kWsPThreads * j;
-  h8 i0, i1, q0, q1;
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+  uint32_t i0[4], i1[4], q0[4], q1[4];
+  const f2v sc = {scale, scale};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {  // samples 2q, 2q + 1: (re, im, re, im)
-    const f4 v = w.v[j][q] * scale;
-    const _Float16 a0 = (_Float16)v.x, b0 = (_Float16)v.y, c0 = (_Float16)v.z, d0 = (_Float16)v.w;
-    i0[2 * q] = a0;
-    i0[2 * q + 1] = c0;
-    q0[2 * q] = b0;
-    q0[2 * q + 1] = d0;
-    i1[2 * q] = (_Float16)(v.x - (float)a0);
-    i1[2 * q + 1] = (_Float16)(v.z - (float)c0);
-    q1[2 * q] = (_Float16)(v.y - (float)b0);
-    q1[2 * q + 1] = (_Float16)(v.w - (float)d0);
+    // packed math on the natural (re, im) register pairs; the I / Q pairing happens in the
+    // two-source f16 conversions, so no register moves: 12 VALU per two samples
+    const f2v s0 = f2v{w.v[j][q].x, w.v[j][q].y} * sc;
+    const f2v s1 = f2v{w.v[j][q].z, w.v[j][q].w} * sc;
+    const h2v hi = __builtin_convertvector(f2v{s0.x, s1.x}, h2v);  // re0, re1
+    const h2v hq = __builtin_convertvector(f2v{s0.y, s1.y}, h2v);  // im0, im1
+    const f2v r0 = s0 - f2v{(float)hi.x, (float)hq.x};
+    const f2v r1 = s1 - f2v{(float)hi.y, (float)hq.y};
+    i0[q] = __builtin_bit_cast(uint32_t, hi);
+    q0[q] = __builtin_bit_cast(uint32_t, hq);
+    i1[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2v{r0.x, r1.x}, h2v));
+    q1[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2v{r0.y, r1.y}, h2v));
   }
   const int off = 16 * cfPhys(g < Wl ? g : a.Wu, a.padShift);
-  *reinterpret_cast<h8*>(planes + off) = i0;
-  *reinterpret_cast<h8*>(planes + a.planeStride + off) = q0;
-  *reinterpret_cast<h8*>(planes + 2 * a.planeStride + off) = i1;
-  *reinterpret_cast<h8*>(planes + 3 * a.planeStride + off) = q1;
+  *reinterpret_cast<uint4*>(planes + off) = uint4{i0[0], i0[1], i0[2], i0[3]};
+  *reinterpret_cast<uint4*>(planes + a.planeStride + off) = uint4{q0[0], q0[1], q0[2], q0[3]};
+  *reinterpret_cast<uint4*>(planes + 2 * a.planeStride + off) = uint4{i1[0], i1[1], i1[2], i1[3]};
+  *reinterpret_cast<uint4*>(planes + 3 * a.planeStride + off) = uint4{q1[0], q1[1], q1[2], q1[3]};
 }
 
 // Producer-local statistics of a window (as cfStatsLocal over the producer threads).
@@ -775,26 +780,27 @@ template <int G>
 __device__ __forceinline__ void wsStatsLocal(int Wl, const CfWindow<G>& w, int ptid, WsCtl* c, int parity) {
   const int lane = ptid & (kWave - 1);
   const int pw = ptid >> 6;
-  float m = 0.0f;
-  float bmin = INFINITY;
-  f4 probe = f4{};
+  // on the bit patterns of |x|: a NaN pattern exceeds +inf's, so M > 3e38 (or NaN) sends a tile
+  // holding a non-finite sample to the direct path without a separate probe
+  uint32_t mu = 0, bminu = 0x7f800000u;
 #pragma unroll
   for (int j = 0; j < G; ++j) {
-    float um = 0.0f;  // units past Wl read as zeros: no effect on either statistic
+    uint32_t um = 0;  // units past Wl read as zeros: no effect on either statistic
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f4 v = w.v[j][q];
-      probe += v * 0.0f;
-      um = fmaxf(um, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      const uint32_t a0 = __builtin_bit_cast(uint32_t, v.x) & 0x7fffffffu;
+      const uint32_t a1 = __builtin_bit_cast(uint32_t, v.y) & 0x7fffffffu;
+      const uint32_t a2 = __builtin_bit_cast(uint32_t, v.z) & 0x7fffffffu;
+      const uint32_t a3 = __builtin_bit_cast(uint32_t, v.w) & 0x7fffffffu;
+      um = max(max(um, a0), max(max(a1, a2), a3));
     }
-    const float bm = dppMax8(um);  // 64-sample block = 8 consecutive units = 8 consecutive lanes
-    m = fmaxf(m, um);
-    if (bm > 0.0f) bmin = fminf(bmin, bm);
+    const uint32_t bm = dppMax8u(um);  // 64-sample block = 8 consecutive units = 8 consecutive lanes
+    mu = max(mu, um);
+    if (bm > 0) bminu = min(bminu, bm);
   }
-  const float pr = (probe.x + probe.y) + (probe.z + probe.w);
-  if (pr != pr) m = INFINITY;
-  m = waveMaxNonNeg(m);
-  bmin = waveMinNonNeg(bmin);
+  const float m = __builtin_bit_cast(float, waveMaxU(mu));
+  const float bmin = __builtin_bit_cast(float, waveMinU(bminu));
   if (lane == 0) {
     c->stat[parity][0][pw] = m;
     c->stat[parity][1][pw] = bmin;
@@ -865,7 +871,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
 #if GSDR_CF_EXPERIMENT & 32
   const uint64_t tStart = __builtin_amdgcn_s_memtime();
 #define WS_STAMP_END() \
-  if (lane == 0) gWsStamp[blockIdx.x * 12 + wave][1] += __builtin_amdgcn_s_memtime() - tStart
+  if (lane == 0) gWsStamp[blockIdx.x * 16 + wave][1] += __builtin_amdgcn_s_memtime() - tStart
 #else
 #define WS_STAMP_END() (void)0
 #endif
@@ -1364,7 +1370,7 @@ hipError_t launchI8DecKS(const I8DecArgs& a, size_t lds, int grid, int epi, hipS
 hipError_t wsReadStamps(unsigned long long* host) {
 #if GSDR_CF_EXPERIMENT & 32
   hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(gWsStamp), sizeof(gWsStamp));
-  static unsigned long long zeros[256 * 12][2];
+  static unsigned long long zeros[256 * 16][2];
   if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(gWsStamp), zeros, sizeof(gWsStamp));
   return e;
 #else

@@ -50,6 +50,37 @@ __device__ __forceinline__ float dppMin8(float v) {
   v = fminf(v, dppF<0xB1>(v));
   return fminf(v, dppF<0x4E>(v));
 }
+// The same on unsigned words (bit patterns of |x|: they order like the values, and NaN patterns
+// sort above +inf, so a max over them also flags non-finite samples). bound_ctrl lets the
+// compiler fold each DPP move into the max.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppU(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t dppMax8u(uint32_t v) {
+  v = max(v, dppU<0x141>(v));
+  v = max(v, dppU<0xB1>(v));
+  return max(v, dppU<0x4E>(v));
+}
+__device__ __forceinline__ uint32_t waveMaxU(uint32_t v) {
+  v = dppMax8u(v);
+  v = max(v, dppU<0x140>(v));
+  uint32_t m = __builtin_amdgcn_readlane(v, 0);
+  m = max(m, (uint32_t)__builtin_amdgcn_readlane(v, 16));
+  m = max(m, (uint32_t)__builtin_amdgcn_readlane(v, 32));
+  return max(m, (uint32_t)__builtin_amdgcn_readlane(v, 48));
+}
+__device__ __forceinline__ uint32_t waveMinU(uint32_t v) {
+  v = min(v, dppU<0x141>(v));
+  v = min(v, dppU<0xB1>(v));
+  v = min(v, dppU<0x4E>(v));
+  v = min(v, dppU<0x140>(v));
+  uint32_t m = __builtin_amdgcn_readlane(v, 0);
+  m = min(m, (uint32_t)__builtin_amdgcn_readlane(v, 16));
+  m = min(m, (uint32_t)__builtin_amdgcn_readlane(v, 32));
+  return min(m, (uint32_t)__builtin_amdgcn_readlane(v, 48));
+}
+
 // wave-wide max / min of NON-NEGATIVE floats (+inf allowed, no NaN): 8-lane groups by DPP, the
 // rows' halves by row_mirror, the four rows through SGPRs (bit patterns order like the values)
 __device__ __forceinline__ float waveMaxNonNeg(float v) {

@@ -43,7 +43,7 @@ int main() {
   struct Shape { const char* name; size_t n, T, D; } shapes[] = {{"c3", (1u << 28) - 6, 1023, 10},
                                                                  {"c4", 1u << 26, 1023, 1}};
   struct V { const char* name; LaunchFn fn; StampFn st; } vars[] = {VARIANT_TABLE};
-  static unsigned long long stamps[256 * 12][2];
+  static unsigned long long stamps[256 * 16][2];
   const int nv = sizeof(vars) / sizeof(vars[0]);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -77,15 +77,15 @@ int main() {
       hipDeviceSynchronize();
       if (v.st(&stamps[0][0]) == hipSuccess) {
         // per role: mean over blocks of (wait cycles, total cycles) of waves 0-7 (consumers) and
-        // 8-11 (producers)
+        // 8-15 (producers)
         double w[2] = {0, 0}, t[2] = {0, 0};
         for (int b = 0; b < 256; ++b)
-          for (int wv = 0; wv < 12; ++wv) {
-            w[wv >= 8] += stamps[b * 12 + wv][0];
-            t[wv >= 8] += stamps[b * 12 + wv][1];
+          for (int wv = 0; wv < 16; ++wv) {
+            w[wv >= 8] += stamps[b * 16 + wv][0];
+            t[wv >= 8] += stamps[b * 16 + wv][1];
           }
         printf("   stamps: consumers wait %.0f of %.0f cycles/wave; producers wait %.0f of %.0f\n", w[0] / 2048,
-               t[0] / 2048, w[1] / 1024, t[1] / 1024);
+               t[0] / 2048, w[1] / 2048, t[1] / 2048);
       }
       hipMemcpy(cur.data(), out, nOut * 4, hipMemcpyDeviceToHost);
       size_t ndiff = 0;
