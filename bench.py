@@ -223,7 +223,9 @@ class AmChainRunner:
         direct-form flops of both FIRs (4 T / D per input sample, 2 Ta / Da per AM sample)."""
         n_rf = self.L // self.D
         n_audio = n_rf // self.Da
-        return 2 * self.L + 4 * n_audio, n_rf * self.T * 4 + n_audio * self.Ta * 2
+        ks = -(-(-(-(31 * self.D + self.T) // 16)) // 8)  # K-steps of 16 per wave, 8 waves
+        # RF stage on the f16 matrix cores (I/Q rows x padded K x 2 tap limbs x 2), audio FIR direct form
+        return 2 * self.L + 4 * n_audio, n_rf * 2 * (8 * ks * 16) * 2 * 2 + n_audio * self.Ta * 2
 
 
 def cpu_baseline(wl, seconds_target=8.0):
@@ -267,11 +269,11 @@ def cpu_baseline(wl, seconds_target=8.0):
 
 def kernel_name(chain):
     if isinstance(chain, AmChainRunner):
-        return (f"gsdrAmChain {chain.mode} step graph (firI8DecMfmaKernel RF FIR+AM, audio FIR, history copies; "
+        return (f"gsdrAmChain {chain.mode} step graph (firI8WsKernel RF FIR+AM, audio FIR, history copies; "
                 "HIP events around the whole step)")
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"
-    body = "firI8MfmaKernel" if chain.mfma_int8 else ("firCfF16MfmaKernel" if chain.mfma_cf else "firLdsKernel")
+    body = "firI8MfmaKernel" if chain.mfma_int8 else ("firCfWsKernel" if chain.mfma_cf else "firLdsKernel")
     return f"{entry} ({body})"
 
 
@@ -378,6 +380,10 @@ def main():
                             {"kind": "f16 MFMA (2x2 limbs with per-tile scale, 3 products, fp32 accumulate)",
                              "achieved_tflops": achieved_t, "peak_tflops": F16_PEAK_TFLOPS,
                              "frac": achieved_t / F16_PEAK_TFLOPS, "flops_per_launch": ops_} if chain.mfma_cf else
+                            {"kind": "f16 MFMA (RF FIR, 2 tap limbs, padded Toeplitz K) + fp32 VALU (audio FIR, "
+                                     "direct form)", "achieved_tflops": achieved_t, "peak_tflops": F16_PEAK_TFLOPS,
+                             "frac": achieved_t / F16_PEAK_TFLOPS, "flops_per_launch": ops_}
+                            if isinstance(chain, AmChainRunner) else
                             {"kind": "fp32 VALU FMA", "achieved_tflops": achieved_t,
                              "peak_tflops": FP32_PEAK_TFLOPS, "frac": achieved_t / FP32_PEAK_TFLOPS,
                              "flops_per_launch": ops_}),

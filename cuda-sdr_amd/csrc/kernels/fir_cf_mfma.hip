@@ -849,6 +849,126 @@ __device__ __forceinline__ void wsProducerTile(const CfFirArgs& a, int Wl, int8_
   wsSignal(&c->pstat, lane);
 }
 
+// Consumer waves of the wave-specialised kernels (cf32: 4 planes per set, 3 products; int8 IQ:
+// 2 planes, 2 products, no direct tiles). `part` first holds the staged taps (consumers turn them
+// into B fragments), then the partial accumulators.
+template <int KS, int EPI, bool I8>
+__device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, float* part, WsCtl* c, int sh, int t0,
+                                            int n, int tid) {
+  constexpr int NP = I8 ? 2 : 4;
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int D = a.D;
+  const int off0 = 31 * D;
+  const int half = lane >> 5;
+  const int col = lane & 31;
+  h8 bh[kCfMaxKS], bl[kCfMaxKS];
+#pragma unroll
+  for (int s = 0; s < kCfMaxKS; ++s) {
+    if (s < KS) {
+      const int kap = 16 * (wave * KS + s) + 8 * half;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float hs = ldexpf(part[off0 + kap + e - col * D], sh);
+        const _Float16 hi = (_Float16)hs;
+        bh[s][e] = hi;
+        bl[s][e] = (_Float16)(hs - (float)hi);
+      }
+    } else {
+      bh[s] = h8{};
+      bl[s] = h8{};
+    }
+  }
+  // no barrier past this point (the roles diverge): the tap staging area becomes the partial-sum
+  // area once every consumer wave has its fragments (tapsRead, awaited before the first partials)
+  wsSignal(&c->tapsRead, lane);
+
+  const int arow = lane & 15;
+  const int comp = (lane >> 4) & 1;
+  const int uRow = 4 * D * arow + half;
+  for (int i = 0; i < n; ++i) {
+    const int set = i & 1;
+    const int tile = t0 + i;
+    wsWait(c, &c->planesFull[set], kWsProducers * ((i >> 1) + 1));
+    const int mode = waveUniform(c->mode[set]);
+    if (!I8 && mode == kWsDirect) {
+      wsSignal(&c->planesFree[set], lane);
+      directTile<EPI>(a, tile, tid);
+      // the partial hand-off counters advance as for any tile (they keep the waves within a tile
+      // of each other, which the count-based waits rely on)
+      wsWait(c, &c->partsFree, kCfWaves * i);
+      wsSignal(&c->partsFull, lane);
+      wsWait(c, &c->partsFull, kCfWaves * (i + 1));
+      wsSignal(&c->partsFree, lane);
+      continue;
+    }
+    const int8_t* pI = smem + set * NP * a.planeStride + comp * a.planeStride;
+    v16f acc = v16f{};
+    // A fragments one K-step ahead; the empty asm keeps the scheduler from hoisting more reads
+    // (168 VGPRs: the tap fragments already hold 88). int8 input: one plane per component (x'
+    // exact in f16), cf32: two limbs.
+    h8 x0, x1 = h8{};
+    {
+      const int off = 16 * cfPhys(uRow + 2 * wave * KS, a.padShift);
+      x0 = *reinterpret_cast<const h8*>(pI + off);
+      if (!I8) x1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
+    }
+#pragma unroll
+    for (int s = 0; s < kCfMaxKS; ++s) {
+      if (s < KS) {
+        h8 n0 = x0, n1 = x1;
+        if (s + 1 < KS) {
+          const int off = 16 * cfPhys(uRow + 2 * (wave * KS + s + 1), a.padShift);
+          n0 = *reinterpret_cast<const h8*>(pI + off);
+          if (!I8) n1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
+        }
+        asm volatile("" ::: "memory");
+        if (GSDR_CF_EXPERIMENT & 2) {
+          acc[s] += (float)x0[0] + (float)x1[1];
+        } else {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
+          if (!I8) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
+        }
+        x0 = n0;
+        x1 = n1;
+      }
+    }
+    wsSignal(&c->planesFree[set], lane);  // this wave's A reads are complete
+    wsWait(c, &c->partsFree, kCfWaves * i);  // every wave has read tile i - 1's partials
+    if (i == 0) wsWait(c, &c->tapsRead, kCfWaves);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
+    wsSignal(&c->partsFull, lane);
+    wsWait(c, &c->partsFull, kCfWaves * (i + 1));
+    if (!(GSDR_CF_EXPERIMENT & 8)) {
+      // wave w finishes accumulator register w (I) / w + 8 (Q), as the synchronous kernels
+      float yi = 0.0f, yq = 0.0f;
+#pragma unroll
+      for (int v = 0; v < kCfWaves; ++v) {
+        yi += part[(v * 16 + wave) * kWave + lane];
+        yq += part[(v * 16 + wave + 8) * kWave + lane];
+      }
+      wsSignal(&c->partsFree, lane);
+      const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * half;
+      const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
+      if (k < a.nOut) {
+        if (I8) {  // the epilogue of firI8DecMfmaKernel: y = acc 2^-sc / 127
+          const float outScale = ldexpf(1.0f / 127.0f, -sh);
+          if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = __builtin_amdgcn_sqrtf(fmaf(yi, yi, yq * yq)) * outScale;
+          else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
+        } else {
+          const float outScale = ldexpf(1.0f, -(mode + sh));
+          if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq}) * outScale;
+          else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
+        }
+      }
+    } else {
+      wsSignal(&c->partsFree, lane);
+    }
+  }
+}
+
 template <int KS, int G, int EPI>
 __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int Wl) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -922,107 +1042,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
     return;
   }
 
-  // ================= consumers =================
-  const int half = lane >> 5;
-  const int col = lane & 31;
-  h8 bh[kCfMaxKS], bl[kCfMaxKS];
-#pragma unroll
-  for (int s = 0; s < kCfMaxKS; ++s) {
-    if (s < KS) {
-      const int kap = 16 * (wave * KS + s) + 8 * half;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float hs = ldexpf(part[off0 + kap + e - col * D], sh);
-        const _Float16 hi = (_Float16)hs;
-        bh[s][e] = hi;
-        bl[s][e] = (_Float16)(hs - (float)hi);
-      }
-    } else {
-      bh[s] = h8{};
-      bl[s] = h8{};
-    }
-  }
-  // no barrier past this point (the roles diverge): the tap staging area becomes the partial-sum
-  // area once every consumer wave has its fragments (tapsRead, awaited before the first partials)
-  wsSignal(&c->tapsRead, lane);
-
-  const int arow = lane & 15;
-  const int comp = (lane >> 4) & 1;
-  const int uRow = 4 * D * arow + half;
-  for (int i = 0; i < n; ++i) {
-    const int set = i & 1;
-    const int tile = t0 + i;
-    wsWait(c, &c->planesFull[set], kWsProducers * ((i >> 1) + 1));
-    const int mode = waveUniform(c->mode[set]);
-    if (mode == kWsDirect) {
-      wsSignal(&c->planesFree[set], lane);
-      directTile<EPI>(a, tile, tid);
-      // the partial hand-off counters advance as for any tile (they keep the waves within a tile
-      // of each other, which the count-based waits rely on)
-      wsWait(c, &c->partsFree, kCfWaves * i);
-      wsSignal(&c->partsFull, lane);
-      wsWait(c, &c->partsFull, kCfWaves * (i + 1));
-      wsSignal(&c->partsFree, lane);
-      continue;
-    }
-    const int8_t* pI = smem + set * 4 * a.planeStride + comp * a.planeStride;
-    v16f acc = v16f{};
-    // A fragments one K-step ahead; the empty asm keeps the scheduler from hoisting more reads
-    // (168 VGPRs: the tap fragments already hold 88)
-    h8 x0, x1;
-    {
-      const int off = 16 * cfPhys(uRow + 2 * wave * KS, a.padShift);
-      x0 = *reinterpret_cast<const h8*>(pI + off);
-      x1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
-    }
-#pragma unroll
-    for (int s = 0; s < kCfMaxKS; ++s) {
-      if (s < KS) {
-        h8 n0 = x0, n1 = x1;
-        if (s + 1 < KS) {
-          const int off = 16 * cfPhys(uRow + 2 * (wave * KS + s + 1), a.padShift);
-          n0 = *reinterpret_cast<const h8*>(pI + off);
-          n1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
-        }
-        asm volatile("" ::: "memory");
-        if (GSDR_CF_EXPERIMENT & 2) {
-          acc[s] += (float)x0[0] + (float)x1[1];
-        } else {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
-        }
-        x0 = n0;
-        x1 = n1;
-      }
-    }
-    wsSignal(&c->planesFree[set], lane);  // this wave's A reads are complete
-    wsWait(c, &c->partsFree, kCfWaves * i);  // every wave has read tile i - 1's partials
-    if (i == 0) wsWait(c, &c->tapsRead, kCfWaves);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
-    wsSignal(&c->partsFull, lane);
-    wsWait(c, &c->partsFull, kCfWaves * (i + 1));
-    if (!(GSDR_CF_EXPERIMENT & 8)) {
-      // wave w finishes accumulator register w (I) / w + 8 (Q), as the synchronous kernels
-      float yi = 0.0f, yq = 0.0f;
-#pragma unroll
-      for (int v = 0; v < kCfWaves; ++v) {
-        yi += part[(v * 16 + wave) * kWave + lane];
-        yq += part[(v * 16 + wave + 8) * kWave + lane];
-      }
-      wsSignal(&c->partsFree, lane);
-      const float outScale = ldexpf(1.0f, -(mode + sh));
-      const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * half;
-      const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
-      if (k < a.nOut) {
-        if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq}) * outScale;
-        else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
-      }
-    } else {
-      wsSignal(&c->partsFree, lane);
-    }
-  }
+  wsConsumers<KS, EPI, false>(a, smem, part, c, sh, t0, n, tid);
   WS_STAMP_END();
 }
 #undef WS_STAMP_END
@@ -1197,6 +1217,152 @@ __global__ __launch_bounds__(kCfThreads, 1) void firI8DecMfmaKernel(I8DecArgs a)
   }
 }
 
+// ---- wave-specialised int8 IQ decimating kernel (default for firI8DecMfma) --------------------
+//
+// firCfWsKernel's roles and hand-offs with the int8 window: producers load 16-byte units (8 IQ
+// samples) plus the following dword (a 2-byte-misaligned input straddles it), funnel-shift by the
+// misalignment and convert to the exact f16 I / Q planes (no statistics, no direct tiles);
+// consumers run two products per K-step and firI8DecMfmaKernel's epilogue (bit-identical).
+
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+template <int G>
+struct I8WsWindow {
+  u4v q[G];       // the unit's 16 bytes from the dword holding its first byte
+  uint32_t e[G];  // the next dword
+};
+
+__device__ __forceinline__ i4v wsI8TileRsrc(const I8DecArgs& a, int tile, bool valid) {
+  const int64_t first = (int64_t)tile * kCfTileOut * a.D * 2;  // bytes from iq4
+  const int64_t total = (2 * a.nIn + a.sub + 3) & ~(int64_t)3;  // whole dwords holding input bytes
+  const int64_t left = valid ? total - first : 0;
+  const int64_t bytes = left < 0x7fffffff ? left : 0x7fffffff;
+  const uint64_t base = reinterpret_cast<uint64_t>(a.iq4 + first);
+  i4v r;
+  r.x = waveUniform((int)(uint32_t)base);
+  r.y = waveUniform((int)((base >> 32) & 0xffffu));
+  r.z = waveUniform((int)bytes);
+  r.w = 0x00020000;
+  return r;
+}
+
+template <int G>
+__device__ __forceinline__ void wsI8LoadGroup(i4v rsrc, int Wl, int ptid, int j, I8WsWindow<G>& w) {
+  const int g = ptid + kWsPThreads * j;
+  const int voff = g < Wl ? 16 * g : 0x7ffffff0;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(w.q[j]) : "v"(voff), "s"(rsrc) : "memory");
+  asm volatile("buffer_load_dword %0, %1, %2, 0 offen offset:16" : "=v"(w.e[j]) : "v"(voff), "s"(rsrc) : "memory");
+}
+
+template <int N, int G>
+__device__ __forceinline__ void wsI8WaitWindow(I8WsWindow<G>& w) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    asm volatile("" : "+v"(w.q[j]));
+    asm volatile("" : "+v"(w.e[j]));
+  }
+}
+
+// Producer, tile i: wCur holds tile i's window (complete after the wait), wNext tile i + 1's.
+template <int G>
+__device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
+                                                 int i, int ptid, I8WsWindow<G>& wCur) {
+  const int lane = ptid & (kWave - 1);
+  const int set = i & 1;
+  wsI8WaitWindow<2 * G>(wCur);
+  wsWait(c, &c->planesFree[set], kCfWaves * (i >> 1));
+  int8_t* planes = smem + set * 2 * a.planeStride;
+  const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int g = ptid + kWsPThreads * j;
+    const uint32_t words[4] = {__builtin_amdgcn_alignbyte(wCur.q[j].y, wCur.q[j].x, a.sub),
+                               __builtin_amdgcn_alignbyte(wCur.q[j].z, wCur.q[j].y, a.sub),
+                               __builtin_amdgcn_alignbyte(wCur.q[j].w, wCur.q[j].z, a.sub),
+                               __builtin_amdgcn_alignbyte(wCur.e[j], wCur.q[j].w, a.sub)};
+    uint4 iu, qu;
+    int8IqToF16Units(words, iu, qu);
+    const int off = 16 * cfPhys(g < Wl ? g : a.Wu, a.padShift);  // spare unit Wu: never read
+    *reinterpret_cast<uint4*>(planes + off) = iu;
+    *reinterpret_cast<uint4*>(planes + a.planeStride + off) = qu;
+    wsI8LoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
+  }
+  if (ptid == 0) c->mode[set] = 0;
+  wsSignal(&c->planesFull[set], lane);
+}
+
+template <int KS, int G, int EPI>
+__global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int Wl) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  float* part = reinterpret_cast<float*>(smem + 4 * a8.planeStride);
+  __shared__ WsCtl ctl;
+  __shared__ float waveMax[kCfWaves + kWsProducers];
+  WsCtl* c = &ctl;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int D = a8.D, T = a8.T;
+
+  const int q = a8.tiles / (int)gridDim.x, r = a8.tiles % (int)gridDim.x;
+  const int t0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
+  const int n = q + ((int)blockIdx.x < r ? 1 : 0);
+  if (n <= 0) return;
+
+  // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), block max; zero both plane sets --------
+  if (tid < (int)(sizeof(WsCtl) / 4)) reinterpret_cast<int*>(c)[tid] = 0;
+  const int off0 = 31 * D;
+  const int span = off0 + 128 * KS;
+  float hm = 0.0f;
+  for (int i = tid; i < span; i += kWsThreads) {
+    const int j = i - off0;
+    const float h = (j >= 0 && j < T) ? a8.taps[j] : 0.0f;
+    part[i] = h;
+    hm = fmaxf(hm, fabsf(h));
+  }
+  for (int i = tid; i < 4 * a8.planeStride / 16; i += kWsThreads) reinterpret_cast<uint4*>(smem)[i] = uint4{0, 0, 0, 0};
+  hm = waveMaxNonNeg(hm);
+  if (lane == 0) waveMax[wave] = hm;
+  __syncthreads();
+  float hMax = waveMax[0];
+#pragma unroll
+  for (int v = 1; v < kCfWaves + kWsProducers; ++v) hMax = fmaxf(hMax, waveMax[v]);
+  const int sh = hMax > 0.0f ? 14 - ilogbf(hMax) : 0;  // max |h 2^sh| in [2^14, 2^15)
+
+  if (wave >= kCfWaves) {
+    const int ptid = tid - kCfThreads;
+    I8WsWindow<G> wA, wB;
+    const i4v r0 = wsI8TileRsrc(a8, t0, true);
+#pragma unroll
+    for (int j = 0; j < G; ++j) wsI8LoadGroup<G>(r0, Wl, ptid, j, wA);
+    const i4v r1 = wsI8TileRsrc(a8, t0 + 1, n > 1);
+#pragma unroll
+    for (int j = 0; j < G; ++j) wsI8LoadGroup<G>(r1, Wl, ptid, j, wB);
+    for (int i = 0;; i += 2) {
+      wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA);
+      if (i + 1 >= n) break;
+      wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB);
+      if (i + 2 >= n) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+  CfFirArgs a{};
+  a.taps = a8.taps;
+  a.out = a8.out;
+  a.nOut = a8.nOut;
+  a.nIn = a8.nIn;
+  a.T = a8.T;
+  a.D = a8.D;
+  a.KS = a8.KS;
+  a.tiles = a8.tiles;
+  a.Wu = a8.Wu;
+  a.padShift = a8.padShift;
+  a.planeStride = a8.planeStride;
+  wsConsumers<KS, EPI, true>(a, smem, part, c, sh, t0, n, tid);
+}
+
 // ---- host side ------------------------------------------------------------------------------
 
 namespace {
@@ -1354,6 +1520,47 @@ hipError_t launchCfWsAny(const CfFirArgs& a, int Wl, size_t lds, int grid, int e
   }
 }
 
+template <int KS, int G, int EPI>
+hipError_t launchI8WsG(const I8DecArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
+  auto kernel = &firI8WsKernel<KS, G, EPI>;
+  static std::once_flag once;
+  static hipError_t attrErr = hipSuccess;
+  std::call_once(once, [kernel] {
+    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kCfDynLdsMax);
+  });
+  if (attrErr != hipSuccess) return attrErr;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWsThreads), lds, stream, a, Wl);
+  return hipGetLastError();
+}
+
+template <int KS>
+hipError_t launchI8WsKS(const I8DecArgs& a, int Wl, size_t lds, int grid, int epi, hipStream_t stream) {
+  const int G = (Wl + kWsPThreads - 1) / kWsPThreads;
+  switch (G) {
+    case 1: return epi == kEpiAm ? launchI8WsG<KS, 1, kEpiAm>(a, Wl, lds, grid, stream) : launchI8WsG<KS, 1, kEpiComplex>(a, Wl, lds, grid, stream);
+    case 2: return epi == kEpiAm ? launchI8WsG<KS, 2, kEpiAm>(a, Wl, lds, grid, stream) : launchI8WsG<KS, 2, kEpiComplex>(a, Wl, lds, grid, stream);
+    case 3: return epi == kEpiAm ? launchI8WsG<KS, 3, kEpiAm>(a, Wl, lds, grid, stream) : launchI8WsG<KS, 3, kEpiComplex>(a, Wl, lds, grid, stream);
+    default: return epi == kEpiAm ? launchI8WsG<KS, 4, kEpiAm>(a, Wl, lds, grid, stream) : launchI8WsG<KS, 4, kEpiComplex>(a, Wl, lds, grid, stream);
+  }
+}
+
+hipError_t launchI8WsAny(const I8DecArgs& a, int Wl, size_t lds, int grid, int epi, hipStream_t stream) {
+  switch (a.KS) {
+    case 1: return launchI8WsKS<1>(a, Wl, lds, grid, epi, stream);
+    case 2: return launchI8WsKS<2>(a, Wl, lds, grid, epi, stream);
+    case 3: return launchI8WsKS<3>(a, Wl, lds, grid, epi, stream);
+    case 4: return launchI8WsKS<4>(a, Wl, lds, grid, epi, stream);
+    case 5: return launchI8WsKS<5>(a, Wl, lds, grid, epi, stream);
+    case 6: return launchI8WsKS<6>(a, Wl, lds, grid, epi, stream);
+    case 7: return launchI8WsKS<7>(a, Wl, lds, grid, epi, stream);
+    case 8: return launchI8WsKS<8>(a, Wl, lds, grid, epi, stream);
+    case 9: return launchI8WsKS<9>(a, Wl, lds, grid, epi, stream);
+    case 10: return launchI8WsKS<10>(a, Wl, lds, grid, epi, stream);
+    default: return launchI8WsKS<11>(a, Wl, lds, grid, epi, stream);
+  }
+}
+
 template <int KS>
 hipError_t launchI8DecKS(const I8DecArgs& a, size_t lds, int grid, int epi, hipStream_t stream) {
   const int G = (a.Wu + kCfThreads - 1) / kCfThreads;
@@ -1485,6 +1692,35 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
   a.tiles = (int32_t)tiles;
   a.Wu = 60 * a.D + 16 * a.KS;
+#ifdef GSDR_FORCE_POLICY
+  const uint32_t policy = GSDR_FORCE_POLICY;
+#else
+  const uint32_t policy = kernelPolicy();
+#endif
+  const int grid = (int)(tiles < 256 ? tiles : 256);
+  // wave-specialised unless GSDR_POLICY_NO_WS (two plane sets of the int8 window always fit)
+  const int Wl = std::min(a.Wu, (511 * a.D + a.T + 7) / 8);
+  if ((policy & GSDR_POLICY_NO_WS) == 0 && Wl <= 4 * kWsPThreads) {
+    static std::mutex wsMu;
+    static int wsD = -1, wsKS = -1;
+    static CfLayout wsLayout{};
+    CfLayout lay;
+    {
+      std::lock_guard<std::mutex> lock(wsMu);
+      if (wsD != a.D || wsKS != a.KS) {
+        wsLayout = cfPlaneLayout(a.D, a.KS, a.Wu, 4);
+        wsD = a.D;
+        wsKS = a.KS;
+      }
+      lay = wsLayout;
+    }
+    if (lay.planeStride != 0) {
+      a.padShift = lay.padShift;
+      a.planeStride = lay.planeStride;
+      const size_t lds = 4 * (size_t)a.planeStride + kCfPartialBytes;
+      if (lds <= (size_t)kCfDynLdsMax) return launchI8WsAny(a, Wl, lds, grid, epi, stream);
+    }
+  }
   static std::mutex mu;
   static int cachedD = -1, cachedKS = -1;
   static CfLayout cached{};
@@ -1500,7 +1736,6 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
   }
   const size_t lds = 2 * (size_t)a.planeStride + kCfPartialBytes;
   if (a.planeStride == 0 || lds > (size_t)kCfDynLdsMax) return hipErrorInvalidValue;
-  const int grid = (int)(tiles < 256 ? tiles : 256);
   switch (a.KS) {
     case 1: return launchI8DecKS<1>(a, lds, grid, epi, stream);
     case 2: return launchI8DecKS<2>(a, lds, grid, epi, stream);

@@ -256,6 +256,31 @@ def test_int8_decimating_mfma_path(ops, orc, T, D, n_out):
     assert np.all(np.abs(y.astype(np.complex128) - y_valu) <= 2 * FIR_TOL * bound + 1e-30)
 
 
+@pytest.mark.parametrize("T,D,n_out,off", [(1023, 10, 400_000, 0), (1023, 10, 130_001, 2), (255, 4, 200_000, 6),
+                                           (1346, 2, 150_000, 0), (64, 3, 90_000, 4)])
+def test_int8_decimating_wave_specialised_bit_exact(ops, orc, T, D, n_out, off):
+    """The wave-specialised int8 decimating kernel (producer waves convert, consumer waves run the
+    MFMAs) is bit-identical to the barrier-synchronous one, at several tiles per block and at
+    2-byte-misaligned inputs; and within tolerance of float64 on a prefix."""
+    rng = np.random.default_rng(T + D + off)
+    n_in = (n_out - 1) * D + T
+    iq = rng.integers(-128, 128, size=2 * n_in + off).astype(np.int8)
+    taps = orc.lowpass_taps(T, 0.4 / D).astype(np.float32)
+    iq_d, taps_d = _dev(iq)[off:], _dev(taps)
+    for am in (False, True):
+        y_ws = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=am))
+        prev = ops.set_kernel_policy(ops.POLICY_NO_WS)
+        try:
+            y_sync = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=am))
+        finally:
+            ops.set_kernel_policy(prev)
+        assert y_ws.tobytes() == y_sync.tobytes(), ("i8-ws-vs-sync", T, D, n_out, off, am)
+    m = min(n_out, 5000)
+    x = orc.int8_to_float(iq[off: off + 2 * ((m - 1) * D + T)]).view(np.complex64)
+    y64, bound = orc.fir_f64(taps, x, D, m)
+    _check_fir(_host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))[:m], y64, bound, ("i8-ws", T, D, off))
+
+
 def test_int8_decimating_mfma_misaligned(ops, orc):
     """Any sample-aligned input takes the MFMA kernel (dword loads + byte funnel shift)."""
     rng = np.random.default_rng(78)

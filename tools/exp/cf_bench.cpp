@@ -78,14 +78,15 @@ int main() {
       if (v.st(&stamps[0][0]) == hipSuccess) {
         // per role: mean over blocks of (wait cycles, total cycles) of waves 0-7 (consumers) and
         // 8-15 (producers)
-        double w[2] = {0, 0}, t[2] = {0, 0};
+        double w[2] = {0, 0}, t[2] = {0, 0}, cnt[2] = {0, 0};
         for (int b = 0; b < 256; ++b)
           for (int wv = 0; wv < 16; ++wv) {
             w[wv >= 8] += stamps[b * 16 + wv][0];
             t[wv >= 8] += stamps[b * 16 + wv][1];
+            cnt[wv >= 8] += stamps[b * 16 + wv][1] != 0;
           }
-        printf("   stamps: consumers wait %.0f of %.0f cycles/wave; producers wait %.0f of %.0f\n", w[0] / 2048,
-               t[0] / 2048, w[1] / 2048, t[1] / 2048);
+        printf("   stamps: consumers wait %.0f of %.0f cycles/wave; producers wait %.0f of %.0f\n", w[0] / cnt[0],
+               t[0] / cnt[0], w[1] / cnt[1], t[1] / cnt[1]);
       }
       hipMemcpy(cur.data(), out, nOut * 4, hipMemcpyDeviceToHost);
       size_t ndiff = 0;
