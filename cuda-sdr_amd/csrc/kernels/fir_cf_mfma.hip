@@ -70,6 +70,7 @@ struct CfFirArgs {
   int32_t Wu;         // window units (8 samples) per tile = 60 D + 16 KS
   int32_t padShift;   // plane unit u lives at u + (u >> padShift)
   int32_t planeStride;  // bytes between the six planes (limb l, component c at 2 l + c)
+  int32_t dbp;          // wave-specialised kernels: two partial-sum buffers
 };
 
 __device__ __forceinline__ int cfPhys(int u, int p) { return u + (u >> p); }
@@ -656,8 +657,8 @@ constexpr int kWsSpinLimit = 1 << 22;                       // s_sleep(1) iterat
 struct WsCtl {
   int planesFull[2];
   int planesFree[2];
-  int partsFull;
-  int partsFree;
+  int partsFull[2];                   // per partial buffer (one buffer: index 0)
+  int partsFree[2];
   int pstat;
   int tapsRead;                       // consumer waves done reading the taps staged in `part`
   int abort;
@@ -849,12 +850,51 @@ __device__ __forceinline__ void wsProducerTile(const CfFirArgs& a, int Wl, int8_
   wsSignal(&c->pstat, lane);
 }
 
+// Consumer wave `wave` reduces accumulator register wave (I) / wave + 8 (Q) of one tile over the
+// eight waves' partials (the synchronous kernels' order) and stores 64 outputs; j is the block-
+// local tile index (its partials: buffer j & 1 when double-buffered, else the single buffer),
+// waited for until every wave has written them. `mode`: the tile's scale exponent, or kWsDirect
+// (outputs already stored).
+template <int EPI, bool I8>
+__device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* part, WsCtl* c, int sh, int tile, int j,
+                                             bool dbp, int mode, int tid) {
+  const int lane = tid & (kWave - 1);
+  const int wave = tid >> 6;
+  const int b = dbp ? (j & 1) : 0;
+  wsWait(c, &c->partsFull[b], kCfWaves * (dbp ? (j >> 1) + 1 : j + 1));
+  if (!(GSDR_CF_EXPERIMENT & 8) && (I8 || mode != kWsDirect)) {
+    const float* pb = part + b * (kCfPartialBytes / 4);
+    float yi = 0.0f, yq = 0.0f;
+#pragma unroll
+    for (int v = 0; v < kCfWaves; ++v) {
+      yi += pb[(v * 16 + wave) * kWave + lane];
+      yq += pb[(v * 16 + wave + 8) * kWave + lane];
+    }
+    wsSignal(&c->partsFree[b], lane);
+    const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * (lane >> 5);
+    const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + (lane & 31);
+    if (k < a.nOut) {
+      if (I8) {  // the epilogue of firI8DecMfmaKernel: y = acc 2^-sc / 127
+        const float outScale = ldexpf(1.0f / 127.0f, -sh);
+        if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = __builtin_amdgcn_sqrtf(fmaf(yi, yi, yq * yq)) * outScale;
+        else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
+      } else {
+        const float outScale = ldexpf(1.0f, -(mode + sh));
+        if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq}) * outScale;
+        else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
+      }
+    }
+  } else {
+    wsSignal(&c->partsFree[b], lane);
+  }
+}
+
 // Consumer waves of the wave-specialised kernels (cf32: 4 planes per set, 3 products; int8 IQ:
 // 2 planes, 2 products, no direct tiles). `part` first holds the staged taps (consumers turn them
 // into B fragments), then the partial accumulators.
 template <int KS, int EPI, bool I8>
 __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, float* part, WsCtl* c, int sh, int t0,
-                                            int n, int tid) {
+                                            int n, int tid, bool dbp) {
   constexpr int NP = I8 ? 2 : 4;
   const int lane = tid & (kWave - 1);
   const int wave = waveUniform(tid >> 6);
@@ -886,6 +926,7 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
   const int arow = lane & 15;
   const int comp = (lane >> 4) & 1;
   const int uRow = 4 * D * arow + half;
+  int prevMode = kWsDirect;
   for (int i = 0; i < n; ++i) {
     const int set = i & 1;
     const int tile = t0 + i;
@@ -894,12 +935,16 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
     if (!I8 && mode == kWsDirect) {
       wsSignal(&c->planesFree[set], lane);
       directTile<EPI>(a, tile, tid);
-      // the partial hand-off counters advance as for any tile (they keep the waves within a tile
-      // of each other, which the count-based waits rely on)
-      wsWait(c, &c->partsFree, kCfWaves * i);
-      wsSignal(&c->partsFull, lane);
-      wsWait(c, &c->partsFull, kCfWaves * (i + 1));
-      wsSignal(&c->partsFree, lane);
+      // the partial hand-off counters advance as for any tile (the count-based waits rely on it)
+      if (dbp) {
+        wsSignal(&c->partsFull[i & 1], lane);
+        if (i >= 1) wsReduceTile<EPI, I8>(a, part, c, sh, tile - 1, i - 1, true, prevMode, tid);
+      } else {
+        wsWait(c, &c->partsFree[0], kCfWaves * i);
+        wsSignal(&c->partsFull[0], lane);
+        wsReduceTile<EPI, I8>(a, part, c, sh, tile, i, false, mode, tid);
+      }
+      prevMode = mode;
       continue;
     }
     const int8_t* pI = smem + set * NP * a.planeStride + comp * a.planeStride;
@@ -935,38 +980,29 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
       }
     }
     wsSignal(&c->planesFree[set], lane);  // this wave's A reads are complete
-    wsWait(c, &c->partsFree, kCfWaves * i);  // every wave has read tile i - 1's partials
-    if (i == 0) wsWait(c, &c->tapsRead, kCfWaves);
+    if (dbp) {
+      // two partial buffers: tile i's partials go to buffer i & 1 and tile i - 1 is reduced right
+      // after, while the other waves may still be finishing tile i (no wait on the slowest wave
+      // before the next tile's MFMAs)
+      const int b = i & 1;
+      wsWait(c, &c->partsFree[b], kCfWaves * (i >> 1));  // tile i - 2 reduced by every wave
+      if (i < 2) wsWait(c, &c->tapsRead, kCfWaves);
+      float* pb = part + b * (kCfPartialBytes / 4);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
-    wsSignal(&c->partsFull, lane);
-    wsWait(c, &c->partsFull, kCfWaves * (i + 1));
-    if (!(GSDR_CF_EXPERIMENT & 8)) {
-      // wave w finishes accumulator register w (I) / w + 8 (Q), as the synchronous kernels
-      float yi = 0.0f, yq = 0.0f;
-#pragma unroll
-      for (int v = 0; v < kCfWaves; ++v) {
-        yi += part[(v * 16 + wave) * kWave + lane];
-        yq += part[(v * 16 + wave + 8) * kWave + lane];
-      }
-      wsSignal(&c->partsFree, lane);
-      const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * half;
-      const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
-      if (k < a.nOut) {
-        if (I8) {  // the epilogue of firI8DecMfmaKernel: y = acc 2^-sc / 127
-          const float outScale = ldexpf(1.0f / 127.0f, -sh);
-          if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = __builtin_amdgcn_sqrtf(fmaf(yi, yi, yq * yq)) * outScale;
-          else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
-        } else {
-          const float outScale = ldexpf(1.0f, -(mode + sh));
-          if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{yi, yq}) * outScale;
-          else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
-        }
-      }
+      for (int k = 0; k < 16; ++k) pb[(wave * 16 + k) * kWave + lane] = acc[k];
+      wsSignal(&c->partsFull[b], lane);
+      if (i >= 1) wsReduceTile<EPI, I8>(a, part, c, sh, tile - 1, i - 1, true, prevMode, tid);
     } else {
-      wsSignal(&c->partsFree, lane);
+      wsWait(c, &c->partsFree[0], kCfWaves * i);  // every wave has read tile i - 1's partials
+      if (i == 0) wsWait(c, &c->tapsRead, kCfWaves);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
+      wsSignal(&c->partsFull[0], lane);
+      wsReduceTile<EPI, I8>(a, part, c, sh, tile, i, false, mode, tid);
     }
+    prevMode = mode;
   }
+  if (dbp && n >= 1) wsReduceTile<EPI, I8>(a, part, c, sh, t0 + n - 1, n - 1, true, prevMode, tid);
 }
 
 template <int KS, int G, int EPI>
@@ -1042,7 +1078,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
     return;
   }
 
-  wsConsumers<KS, EPI, false>(a, smem, part, c, sh, t0, n, tid);
+  wsConsumers<KS, EPI, false>(a, smem, part, c, sh, t0, n, tid, a.dbp != 0);
   WS_STAMP_END();
 }
 #undef WS_STAMP_END
@@ -1063,6 +1099,7 @@ struct I8DecArgs {
   int32_t Wu;         // window units (8 samples = 16 input bytes) per tile = 60 D + 16 KS
   int32_t padShift;
   int32_t planeStride;  // bytes between the I and Q f16 planes
+  int32_t dbp;          // wave-specialised kernel: two partial-sum buffers
 };
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -1360,7 +1397,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
   a.Wu = a8.Wu;
   a.padShift = a8.padShift;
   a.planeStride = a8.planeStride;
-  wsConsumers<KS, EPI, true>(a, smem, part, c, sh, t0, n, tid);
+  a.dbp = a8.dbp;
+  wsConsumers<KS, EPI, true>(a, smem, part, c, sh, t0, n, tid, a8.dbp != 0);
 }
 
 // ---- host side ------------------------------------------------------------------------------
@@ -1636,7 +1674,9 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
     if (lay.planeStride != 0) {
       a.padShift = lay.padShift;
       a.planeStride = lay.planeStride;
-      const size_t lds = 8 * (size_t)a.planeStride + kCfPartialBytes;
+      size_t lds = 8 * (size_t)a.planeStride + 2 * kCfPartialBytes;
+      a.dbp = lds <= (size_t)kCfDynLdsMax;  // double-buffered partials when they fit
+      if (!a.dbp) lds -= kCfPartialBytes;
       if (lds <= (size_t)kCfDynLdsMax) return launchCfWsAny(a, Wl, lds, grid, epi, stream);
     }
   }
@@ -1717,7 +1757,9 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
     if (lay.planeStride != 0) {
       a.padShift = lay.padShift;
       a.planeStride = lay.planeStride;
-      const size_t lds = 4 * (size_t)a.planeStride + kCfPartialBytes;
+      size_t lds = 4 * (size_t)a.planeStride + 2 * kCfPartialBytes;
+      a.dbp = lds <= (size_t)kCfDynLdsMax;
+      if (!a.dbp) lds -= kCfPartialBytes;
       if (lds <= (size_t)kCfDynLdsMax) return launchI8WsAny(a, Wl, lds, grid, epi, stream);
     }
   }
