@@ -7,6 +7,7 @@
 #include <unordered_map>
 
 #include "buffers.h"
+#include "composite.h"
 #include "driver.h"
 #include "filters.h"
 #include "json.h"
@@ -292,36 +293,6 @@ class StubQueueFilterFactory final : public ICudaFilterFactory {
   const char* mName;
   REF_COUNTED(StubQueueFilterFactory);
 };
-class StubFilterDriverFactory final : public IFilterDriverFactory {
- public:
-  Result<Node> create(const char*) noexcept final { GS_OUT_OF_SCOPE("Component"); }
-  Result<IFilterDriver> createFilterDriver() noexcept final { GS_OUT_OF_SCOPE("FilterDriver"); }
-  REF_COUNTED(StubFilterDriverFactory);
-};
-class StubPortRemappingSinkFactory final : public IPortRemappingSinkFactory {
- public:
-  Result<IPortRemappingSink> create() noexcept final { GS_OUT_OF_SCOPE("PortRemappingSink"); }
-  REF_COUNTED(StubPortRemappingSinkFactory);
-};
-class StubPortRemappingSourceFactory final : public IPortRemappingSourceFactory {
- public:
-  Result<IPortRemappingSource> create() noexcept final { GS_OUT_OF_SCOPE("PortRemappingSource"); }
-  REF_COUNTED(StubPortRemappingSourceFactory);
-};
-class StubRfToPcmFactory final : public IRfToPcmAudioFactory {
- public:
-  Result<Node> create(const char*) noexcept final { GS_OUT_OF_SCOPE("RfToPcmAudio"); }
-  Result<Filter> createRfToPcm(float, Modulation, size_t, size_t, float, float, float, float, float, float,
-                               const char*) noexcept final {
-    GS_OUT_OF_SCOPE("RfToPcmAudio");
-  }
-  REF_COUNTED(StubRfToPcmFactory);
-};
-class StubByteCountMonitorFactory final : public IReadByteCountMonitorFactory {
- public:
-  Result<IReadByteCountMonitor> create(Filter*) noexcept final { GS_OUT_OF_SCOPE("ReadByteCountMonitor"); }
-  REF_COUNTED(StubByteCountMonitorFactory);
-};
 class StubDriverToDotFactory final : public IDriverToDiagramFactory {
  public:
   Result<IDriverToDiagram> create() const noexcept final { GS_OUT_OF_SCOPE("DriverToDot"); }
@@ -357,11 +328,11 @@ class Factories final : public IFactories {
         mHackrf(new StubHackrfFactory()),
         mMultiply(new QueueFilterFactory(this, &MultiplyCcc::create)),
         mStepping(new SteppingDriverFactory()),
-        mComponent(new StubFilterDriverFactory()),
-        mRemapSink(new StubPortRemappingSinkFactory()),
-        mRemapSource(new StubPortRemappingSourceFactory()),
-        mRfToPcm(new StubRfToPcmFactory()),
-        mMonitor(new StubByteCountMonitorFactory()),
+        mComponent(newFilterDriverFactory(this)),
+        mRemapSink(newPortRemappingSinkFactory()),
+        mRemapSource(newPortRemappingSourceFactory()),
+        mRfToPcm(newRfToPcmAudioFactory(this)),
+        mMonitor(newReadByteCountMonitorFactory()),
         mDot(new StubDriverToDotFactory()) {}
 
   IResizableBufferFactory* getResizableBufferFactory() noexcept final { return mResizable; }
@@ -585,6 +556,8 @@ GS_EXPORT Status registerDefaultNodeFactories() noexcept {
   FWD_IF_ERR(registerNodeFactory("MultiplyCCC", F->getMultiplyFactory()));
   FWD_IF_ERR(registerNodeFactory("QuadDemod", F->getQuadDemodFactory()));
   FWD_IF_ERR(registerNodeFactory("HipMemcpy", F->getCudaMemcpyFilterFactory()));
+  // extension: the RF -> PCM component by name (the reference only reaches it through IFactories)
+  FWD_IF_ERR(registerNodeFactory("RfToPcmAudio", F->getRfToPcmAudioFactory()));
   return Status_Success;
 }
 

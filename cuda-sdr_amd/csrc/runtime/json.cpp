@@ -1,5 +1,6 @@
 #include "json.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -191,6 +192,76 @@ class JsonParser {
     return true;
   }
 };
+
+namespace {
+void dumpString(const std::string& s, std::string& out) {
+  out += '"';
+  for (const char c : s) {
+    switch (c) {
+      case '"': out += "\\\""; break;
+      case '\\': out += "\\\\"; break;
+      case '\n': out += "\\n"; break;
+      case '\r': out += "\\r"; break;
+      case '\t': out += "\\t"; break;
+      case '\b': out += "\\b"; break;
+      case '\f': out += "\\f"; break;
+      default:
+        if ((unsigned char)c < 0x20) {
+          char buf[8];
+          snprintf(buf, sizeof(buf), "\\u%04x", (unsigned)(unsigned char)c);
+          out += buf;
+        } else {
+          out += c;
+        }
+    }
+  }
+  out += '"';
+}
+
+void dumpValue(const Json& v, std::string& out) {
+  switch (v.type()) {
+    case Json::Type::Null: out += "null"; break;
+    case Json::Type::Bool: out += v.boolean() ? "true" : "false"; break;
+    case Json::Type::Number: {
+      char buf[40];
+      snprintf(buf, sizeof(buf), "%.17g", v.number());
+      out += buf;
+      break;
+    }
+    case Json::Type::String: dumpString(v.string(), out); break;
+    case Json::Type::Array: {
+      out += '[';
+      bool first = true;
+      for (const Json& e : v.array()) {
+        if (!first) out += ',';
+        first = false;
+        dumpValue(e, out);
+      }
+      out += ']';
+      break;
+    }
+    case Json::Type::Object: {
+      out += '{';
+      bool first = true;
+      for (const auto& kv : v.object()) {
+        if (!first) out += ',';
+        first = false;
+        dumpString(kv.first, out);
+        out += ':';
+        dumpValue(kv.second, out);
+      }
+      out += '}';
+      break;
+    }
+  }
+}
+}  // namespace
+
+std::string Json::dump() const {
+  std::string out;
+  dumpValue(*this, out);
+  return out;
+}
 
 bool Json::parse(const char* text, Json& out, std::string& error) {
   out = Json();

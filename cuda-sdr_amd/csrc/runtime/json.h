@@ -15,6 +15,8 @@ class Json {
   enum class Type { Null, Bool, Number, String, Array, Object };
 
   static bool parse(const char* text, Json& out, std::string& error);
+  // Compact JSON text of this value (numbers with 17 significant digits: they parse back exactly).
+  std::string dump() const;
 
   Type type() const { return mType; }
   bool isNull() const { return mType == Type::Null; }

@@ -6,10 +6,15 @@
 // Cases: a linear chain with small preferred sizes (many steps, partial consumption, a FIR-like
 // count rule that retains history), output-size alignment, fan-out of one source port to two
 // sinks (copy through getOutputCopier), a two-input sink fed by two chains, the one-upstream-per-
-// sink-port rule, node naming/iteration, and a source that stops producing.
+// sink-port rule, node naming/iteration, and a source that stops producing. Composite graphs
+// (FilterDriver.cpp, FilterDriverFactory.cpp, PortRemapping*.cpp, ReadByteCountMonitor.cpp): an
+// inner graph behind a FilterDriver driven by an outer SteppingDriver, the same graph built from a
+// JSON "Component" definition (nodes from registered test factories), definition errors, and the
+// read-byte-count monitor.
 #include <gpusdrpipeline/Factories.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <numeric>
@@ -142,7 +147,12 @@ class Adder final : public Filter {
     return mIn[port].request(bytes);
   }
   Status commitBuffer(size_t port, size_t bytes) noexcept final { return port > 1 ? Status_OutOfRange : mIn[port].commit(bytes); }
-  size_t preferredInputBufferSize(size_t) noexcept final { return 40; }
+  // as MultiplyCcc (Multiply.cpp): the lagging port asks for the difference, the leading one for
+  // nothing, so a free-running second input (a tone source) never runs ahead of the first
+  size_t preferredInputBufferSize(size_t port) noexcept final {
+    const size_t mine = mIn[port].pending.size(), other = mIn[1 - port].pending.size();
+    return other > mine ? 4 * (other - mine) : (mine > other ? 0 : 40);
+  }
   size_t getOutputDataSize(size_t) noexcept final { return 4 * std::min(mIn[0].pending.size(), mIn[1].pending.size()); }
   size_t getOutputSizeAlignment(size_t) noexcept final { return 4; }
   IBufferCopier* getOutputCopier(size_t) noexcept final { return F()->getSysMemCopier(); }
@@ -305,6 +315,163 @@ void exhaustedSource() {
   CHECK((sink->mIn.pending == std::vector<int32_t>{3, 6, 9}));
 }
 
+// y[k] = sum_j (x[k D + j] + tone[k D + j]): the FilterDriver case's inner graph on the whole stream
+std::vector<int32_t> compositeExpect(size_t n, int32_t toneStart, size_t T, size_t D) {
+  std::vector<int32_t> x(n);
+  for (size_t i = 0; i < n; ++i) x[i] = (int32_t)i + toneStart + (int32_t)i;
+  return windowSums(x, T, D);
+}
+
+void filterDriverComposite() {
+  // outer: Counter(0..2999) -> [FilterDriver: in.0 -> Adder.0 ; Counter(500..) -> Adder.1 ;
+  //         Adder -> WindowSum(5, 2) -> out.0] -> Collect
+  Ref<IFilterDriver> fd = unwrap(F()->getFilterDriverFactory()->createFilterDriver());
+  Ref<CounterSource> tone = new CounterSource(500 + 4000, 4, 500);  // readOutput materialises what is left
+  Ref<Adder> add = new Adder();
+  Ref<WindowSum> w = new WindowSum(5, 2, 36);
+  THROW_IF_ERR(fd->connect(tone.get(), 0, add.get(), 1));
+  THROW_IF_ERR(fd->connect(add.get(), 0, w.get(), 0));
+  Ref<IPortRemappingSink> in = unwrap(F()->getPortRemappingSinkFactory()->create());
+  Ref<IPortRemappingSource> out = unwrap(F()->getPortRemappingSourceFactory()->create());
+  in->addPortMapping(0, add.get(), 0);
+  out->addPortMapping(0, w.get(), 0);
+  fd->setDriverInput(in.get());
+  fd->setDriverOutput(out.get());
+  THROW_IF_ERR(fd->setupNode(add.get(), "adder"));
+
+  Ref<CounterSource> src = new CounterSource(3000, 4);
+  Ref<Collect> sink = new Collect(44);
+  Ref<ISteppingDriver> d = newDriver();
+  THROW_IF_ERR(d->connect(src.get(), 0, fd.get(), 0));
+  THROW_IF_ERR(d->connect(fd.get(), 0, sink.get(), 0));
+  run(d.get(), [&] { return sink->mIn.pending.size(); });
+  CHECK(sink->mIn.pending == compositeExpect(3000, 500, 5, 2));
+
+  // the inner graph seen from outside: its edges plus the delegate edges, and node attributes
+  int edges = 0, inputAttr = 0;
+  fd->iterateOverConnections(&edges, [](IDriver*, void* c, Source*, size_t, Sink*, size_t) noexcept {
+    ++*static_cast<int*>(c);
+  });
+  CHECK(edges == 4);  // tone -> adder, adder -> window, fd -> in, out -> fd
+  fd->iterateOverNodeAttributes(in.get(), &inputAttr, [](IDriver*, Node*, void* c, const char* k, const char* v) noexcept {
+    if (std::string(k) == "inputNode" && std::string(v) == "true") ++*static_cast<int*>(c);
+  });
+  CHECK(inputAttr == 1);
+  char name[16];
+  bool found = false;
+  CHECK(fd->getNodeName(add.get(), name, sizeof(name), &found) == 5 && found);
+
+  // without delegates the FilterDriver reports InvalidState (FilterDriver.cpp:160-166)
+  Ref<IFilterDriver> bare = unwrap(F()->getFilterDriverFactory()->createFilterDriver());
+  CHECK(bare->requestBuffer(0, 16).status == Status_InvalidState);
+  CHECK(bare->getOutputDataSize(0) == 0);
+}
+
+// Test node factories for the JSON component: parameters are read from the node's OWN definition
+// ("T", "D", "start"), so a factory handed the whole component text would build the wrong node.
+long jsonInt(const char* json, const char* key, long dflt) {
+  const std::string k = std::string("\"") + key + "\":";
+  const char* p = std::strstr(json, k.c_str());
+  return p == nullptr ? dflt : std::strtol(p + k.size(), nullptr, 10);
+}
+
+struct TestFactory final : public INodeFactory {
+  enum Kind { kCounter, kWindow, kAdder } kind;
+  explicit TestFactory(Kind k) : kind(k) {}
+  Result<Node> create(const char* json) noexcept final {
+    if (std::strstr(json, "\"nodes\"") != nullptr) return ERR_RESULT(Status_InvalidArgument);  // whole component
+    Node* n = nullptr;
+    if (kind == kCounter) n = new CounterSource((int32_t)jsonInt(json, "total", 4500), 4, (int32_t)jsonInt(json, "start", 0));
+    if (kind == kWindow) n = new WindowSum((size_t)jsonInt(json, "T", 1), (size_t)jsonInt(json, "D", 1), 36);
+    if (kind == kAdder) n = new Adder();
+    return makeRefResultNonNull<Node>(n);
+  }
+  REF_COUNTED(TestFactory);
+};
+
+void componentFromJson() {
+  THROW_IF_ERR(registerDefaultNodeFactories());  // "Component" is reached by name
+  THROW_IF_ERR(registerNodeFactory("TestCounter", new TestFactory(TestFactory::kCounter)));
+  THROW_IF_ERR(registerNodeFactory("TestWindowSum", new TestFactory(TestFactory::kWindow)));
+  THROW_IF_ERR(registerNodeFactory("TestAdder", new TestFactory(TestFactory::kAdder)));
+  const char* def = R"({"nodes": {"tone": {"type": "TestCounter", "start": 500},
+                                  "adder": {"type": "TestAdder"},
+                                  "window": {"type": "TestWindowSum", "T": 5, "D": 2}},
+                       "connections": [{"source": "tone", "sourcePort": 0, "sink": "adder", "sinkPort": 1},
+                                       {"source": "adder", "target": "window"}],
+                       "inputPorts": [{"exposedPort": 0, "mapped": {"node": "adder", "port": 0}}],
+                       "outputPorts": [{"exposedPort": 0, "mapped": {"node": "window", "port": 0}}]})";
+  Ref<Filter> comp = unwrap(createFilter("Component", def));
+  Ref<CounterSource> src = new CounterSource(3000, 4);
+  Ref<Collect> sink = new Collect(44);
+  Ref<ISteppingDriver> d = newDriver();
+  THROW_IF_ERR(d->connect(src.get(), 0, comp.get(), 0));
+  THROW_IF_ERR(d->connect(comp.get(), 0, sink.get(), 0));
+  run(d.get(), [&] { return sink->mIn.pending.size(); });
+  CHECK(sink->mIn.pending == compositeExpect(3000, 500, 5, 2));
+  // the nodes carry their ids as names in the component's driver
+  IDriver* cd = static_cast<Node*>(comp.get())->asDriver();
+  CHECK(cd != nullptr);
+  int named = 0;
+  if (cd != nullptr)
+    cd->iterateOverNodes(&named, [](IDriver* drv, void* c, Node* n) noexcept {
+      char nm[16];
+      bool f = false;
+      drv->getNodeName(n, nm, sizeof(nm), &f);
+      if (f) ++*static_cast<int*>(c);
+    });
+  CHECK(named == 3);
+
+  // "outputPort": "<id>" (the RF -> PCM form) maps exposed port 0
+  const char* def2 = R"({"nodes": {"w": {"type": "TestWindowSum", "T": 2, "D": 1}},
+                        "inputPorts": [{"exposedPort": 0, "mapped": {"node": "w", "port": 0}}],
+                        "outputPort": "w"})";
+  Ref<Filter> comp2 = unwrap(createFilter("Component", def2));
+  Ref<CounterSource> src2 = new CounterSource(100, 4);
+  Ref<Collect> sink2 = new Collect(64);
+  Ref<ISteppingDriver> d2 = newDriver();
+  THROW_IF_ERR(d2->connect(src2.get(), 0, comp2.get(), 0));
+  THROW_IF_ERR(d2->connect(comp2.get(), 0, sink2.get(), 0));
+  run(d2.get(), [&] { return sink2->mIn.pending.size(); });
+  std::vector<int32_t> x(100);
+  std::iota(x.begin(), x.end(), 0);
+  CHECK(sink2->mIn.pending == windowSums(x, 2, 1));
+}
+
+void componentErrors() {
+  IFilterDriverFactory* f = F()->getFilterDriverFactory();
+  CHECK(f->create("{not json").status == Status_ParseError);
+  CHECK(f->create(R"({"connections": []})").status == Status_ParseError);  // no "nodes"
+  CHECK(f->create(R"({"nodes": {"a": {"T": 3}}})").status == Status_InvalidArgument);  // no type
+  CHECK(f->create(R"({"nodes": {"a": {"type": "NoSuchNodeType"}}})").status == Status_NotFound);
+  CHECK(f->create(R"({"nodes": {"a": {"type": "TestAdder"}},
+                      "connections": [{"source": "a", "sink": "b"}]})")
+            .status == Status_InvalidArgument);  // undefined sink
+  CHECK(f->create(R"({"nodes": {"a": {"type": "TestAdder"}},
+                      "inputPorts": [{"exposedPort": 0, "mapped": {"node": "zz", "port": 0}}]})")
+            .status == Status_NotFound);
+  CHECK(f->create(R"({"nodes": {"a": {"type": "TestCounter"}},
+                      "inputPorts": [{"exposedPort": 0, "mapped": {"node": "a", "port": 0}}]})")
+            .status == Status_InvalidArgument);  // a source is not a sink
+}
+
+void byteCountMonitor() {
+  Ref<CounterSource> src = new CounterSource(1000, 4);
+  Ref<WindowSum> w = new WindowSum(7, 3, 100);
+  Ref<IReadByteCountMonitor> mon = unwrap(F()->getReadByteCountMonitorFactory()->create(w.get()));
+  Ref<Collect> sink = new Collect(48);
+  Ref<ISteppingDriver> d = newDriver();
+  THROW_IF_ERR(d->connect(src.get(), 0, mon.get(), 0));
+  THROW_IF_ERR(d->connect(mon.get(), 0, sink.get(), 0));
+  run(d.get(), [&] { return sink->mIn.pending.size(); });
+  std::vector<int32_t> x(1000);
+  std::iota(x.begin(), x.end(), 0);
+  CHECK(sink->mIn.pending == windowSums(x, 7, 3));
+  CHECK(mon->getByteCountRead(0) == 4 * sink->mIn.pending.size());
+  CHECK(mon->getByteCountRead(3) == 0);
+  CHECK(F()->getReadByteCountMonitorFactory()->create(nullptr).status == Status_InvalidArgument);
+}
+
 void runCase(const char* name, void (*fn)()) {
   const int before = gFailures;
   try {
@@ -325,6 +492,10 @@ int main() {
   runCase("two_inputs", twoInputs);
   runCase("connect_rules_and_names", connectRulesAndNames);
   runCase("exhausted_source", exhaustedSource);
+  runCase("filter_driver_composite", filterDriverComposite);
+  runCase("component_from_json", componentFromJson);
+  runCase("component_errors", componentErrors);
+  runCase("byte_count_monitor", byteCountMonitor);
   printf("%s (%d failures)\n", gFailures == 0 ? "ALL PASS" : "FAILURES", gFailures);
   return gFailures == 0 ? 0 : 1;
 }
