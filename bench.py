@@ -79,6 +79,9 @@ def dist_setup(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}; launch one rank per GPU "
+                         "(torch.distributed.run) or let bench.py spawn them (WORLD_SIZE unset)")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -152,28 +155,39 @@ class ShardedChain:
         if self.kind != "i8":
             self.ring.halo.copy_(self.ring.tail)
 
+    @property
+    def kernel_class(self):
+        x = self.buf if self.single else self.bulk_x
+        return self.ops.fir_kernel_class(x, self.taps, self.D, int8_iq=(self.kind == "i8"))
+
     def timed_bytes_ops(self):
-        """Algorithmic bytes of the timed launch (input read once + output written once) and
-        its arithmetic: f16 MFMA flops for the int8 IQ MFMA kernel, direct-form FMA flops else."""
+        """Algorithmic bytes of the timed launch (input read once + output written once) and the
+        arithmetic the kernel performs: (kind, flops, peak TFLOP/s of the unit it runs on)."""
         g = self.geom
         n = g.outputs if self.single else g.outputs - g.head_outputs
         n_in = (n - 1) * self.D + self.T
         in_bytes = n_in * (2 if self.kind == "i8" else 8)
-        if self.mfma_int8:
-            s = (self.T + 62) // 32  # K-blocks of 32: K = 32 S >= T + 31
-            return in_bytes + n * 4, n * 2 * 2 * 32 * s * 2  # I and Q rows x 2 f16 limbs x K MACs x 2
-        if self.mfma_cf:
-            ks = -(-(-(-(31 * self.D + self.T) // 16)) // 8)  # K-steps of 16 per wave, 8 waves
-            return in_bytes + n * 4, n * 2 * (8 * ks * 16) * 3 * 2  # I/Q rows x K x 3 f16 products x 2
-        return in_bytes + n * 4, n * self.T * 4
+        return in_bytes + n * 4, kernel_compute(self.kernel_class, n, self.T, self.D)
 
-    @property
-    def mfma_int8(self):
-        return self.kind == "i8" and self.D == 1 and self.T <= 129
 
-    @property
-    def mfma_cf(self):
-        return self.kind == "c64" and self.T >= 64 and self.D <= 16 and 31 * self.D + self.T <= 1408
+def kernel_compute(cls, n_out, T, D):
+    """(kind, flops per launch, peak TFLOP/s) of the FIR kernel family `cls` for n_out outputs."""
+    if cls == "fft":
+        Q = -(-T // D)
+        V = 512 - Q + 1
+        blocks = -(-n_out // V)
+        fft = 5 * 512 * 9  # nominal 5 N log2 N per 512-point FFT
+        return ("fp32 FFT fast convolution (polyphase overlap-save, 512-point FFTs; nominal 5 N log2 N)",
+                blocks * (D * fft + D * 512 * 8 + fft), FP32_PEAK_TFLOPS)
+    if cls == "i8-mfma":
+        s = (T + 62) // 32  # K-blocks of 32: K = 32 S >= T + 31
+        return ("f16 MFMA (2 tap limbs, fp32 accumulate)", n_out * 2 * 2 * 32 * s * 2, F16_PEAK_TFLOPS)
+    if cls in ("cf-mfma", "i8-dec-mfma"):
+        ks = -(-(-(-(31 * D + T) // 16)) // 8)  # K-steps of 16 per wave, 8 waves
+        prods = 3 if cls == "cf-mfma" else 2
+        return (f"f16 MFMA (split precision, {prods} products, padded Toeplitz K, fp32 accumulate)",
+                n_out * 2 * (8 * ks * 16) * prods * 2, F16_PEAK_TFLOPS)
+    return ("fp32 VALU FMA (direct form)", n_out * T * 4, FP32_PEAK_TFLOPS)
 
 
 class AmChainRunner:
@@ -201,7 +215,8 @@ class AmChainRunner:
         self.stream = self.chain.torch_stream
         self.geom = None
         self.single = world == 1
-        self.mfma_int8 = self.mfma_cf = False
+        self.kernel_class = ops.fir_kernel_class(self.iq, torch.from_numpy(lowpass(T, cutoff, window)), D,
+                                                 int8_iq=True)
 
     def step(self, ev=None):
         with torch.cuda.stream(self.stream):
@@ -219,31 +234,74 @@ class AmChainRunner:
                 ev[1].record(self.stream)
 
     def timed_bytes_ops(self):
-        """Per timed region (all chunks of a step): int8 input read once + audio written once;
-        direct-form flops of both FIRs (4 T / D per input sample, 2 Ta / Da per AM sample)."""
+        """Per timed region (all chunks of a step): int8 input read once + audio written once; the
+        RF FIR kernel's arithmetic plus the audio FIR's direct-form flops (2 Ta / Da per AM sample)."""
         n_rf = self.L // self.D
         n_audio = n_rf // self.Da
-        ks = -(-(-(-(31 * self.D + self.T) // 16)) // 8)  # K-steps of 16 per wave, 8 waves
-        # RF stage on the f16 matrix cores (I/Q rows x padded K x 2 tap limbs x 2), audio FIR direct form
-        return 2 * self.L + 4 * n_audio, n_rf * 2 * (8 * ks * 16) * 2 * 2 + n_audio * self.Ta * 2
+        kind, fl, peak = kernel_compute(self.kernel_class, n_rf, self.T, self.D)
+        return 2 * self.L + 4 * n_audio, (f"RF: {kind}; audio FIR: fp32 VALU direct form", fl + n_audio * self.Ta * 2,
+                                          peak)
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline: every core this process may run on, capped at the
+    job's CPU share when the launcher states one (OMP_NUM_THREADS; 16 per GPU on the GPU box,
+    whose os.cpu_count() reports the whole machine)."""
+    avail = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        return min(avail, int(share)), avail
+    return avail, avail
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_c1(oracle, threads):
+    """C1 (BASELINE.json configs[0]) in full: CosineSource(fs=1e6, f=12345 Hz) -> 63-tap FF FIR,
+    1 M f32 samples, float32 direct form on the host cores (median of 10 after 2 warm-ups)."""
+    n = 1 << 20
+    delta = float(np.float32(2.0 * np.pi * 12345.0 / 1e6))
+    x = oracle.cosine_f(0.0, float(np.float32(n * delta)), n)
+    taps = oracle.lowpass_taps(63, 0.1)
+    n_out = oracle.fir_output_count(n, 63, 1)
+    for _ in range(2):
+        oracle.fir_ff_f32(taps, x, 1, n_out, threads, baseline=True)
+    ts = []
+    for _ in range(10):
+        t0 = time.perf_counter()
+        oracle.fir_ff_f32(taps, x, 1, n_out, threads, baseline=True)
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts))
+    return {"config": "C1: CosineSource f32 (fs 1e6, 12345 Hz) -> 63-tap FF FIR, 1,048,576 samples, D=1",
+            "value": n / dt / 1e6, "unit": "Msamples/s", "ms": dt * 1e3, "cores": threads}
 
 
 def cpu_baseline(wl, seconds_target=8.0):
-    """Oracle port (float32 direct form, all assigned host cores) on a bounded sample."""
+    """Oracle port (float32 direct form, the host cores) on a bounded sample of workload `wl`,
+    plus the C1 CPU configuration run in full."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # noqa: E402  (cpu_baseline leg only)
     desc, kind, L, T, D, cutoff, window, fs = WORKLOADS[wl]
     taps = lowpass(T, cutoff, window)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, avail = cpu_threads()
     n_out = 1 << 16
     while True:
         n_in = (n_out - 1) * D + T
         if kind == "i8":
             x = oracle.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, 0, n_in)
-            run = lambda: oracle.chain_i8_fc_am_f32(taps, x, D, n_out, threads)  # noqa: E731
+            run = lambda: oracle.chain_i8_fc_am_f32(taps, x, D, n_out, threads, baseline=True)  # noqa: E731
         else:
             x = oracle.synth_wideband_cf32(0xC3, 0.013, 0.31, 0, n_in)
-            run = lambda: oracle.chain_fc_am_f32(taps, x, D, n_out, threads)  # noqa: E731
+            run = lambda: oracle.chain_fc_am_f32(taps, x, D, n_out, threads, baseline=True)  # noqa: E731
         run()  # warm
         t0 = time.perf_counter()
         run()
@@ -260,20 +318,27 @@ def cpu_baseline(wl, seconds_target=8.0):
         "value": (n_out * D) / dt / 1e6,
         "unit": "Msamples/s",
         "cores": threads,
+        "host_cpus": os.cpu_count(),
+        "affinity_cpus": avail,
+        "cpu_model": _cpu_model(),
+        "isa": oracle.baseline_isa(),
         "kind": "port",
         "sample": f"{n_out * D} input samples of the {wl} chain (oracle/gsdr_oracle.c float32 direct form, "
-                  f"{threads} threads, mean of {reps} runs"
+                  f"{threads} threads = {'the job CPU share (OMP_NUM_THREADS)' if threads < avail else 'all cores'}"
+                  f" of {avail} schedulable, mean of {reps} runs"
                   + ("; RF FIR + AM only, the audio FIR is 0.6 % of the flops)" if wl == "c5" else ")"),
+        "c1": cpu_c1(oracle, threads),
     }
 
 
 def kernel_name(chain):
     if isinstance(chain, AmChainRunner):
-        return (f"gsdrAmChain {chain.mode} step graph (firI8WsKernel RF FIR+AM, audio FIR, history copies; "
+        return (f"gsdrAmChain {chain.mode} step graph (RF FIR+AM, audio FIR, history copies; "
                 "HIP events around the whole step)")
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"
-    body = "firI8MfmaKernel" if chain.mfma_int8 else ("firCfWsKernel" if chain.mfma_cf else "firLdsKernel")
+    body = {"fft": "firFftKernel", "i8-mfma": "firI8MfmaKernel", "i8-dec-mfma": "firI8WsKernel",
+            "cf-mfma": "firCfWsKernel", "valu": "firLdsKernel"}[chain.kernel_class]
     return f"{entry} ({body})"
 
 
@@ -288,17 +353,46 @@ def load_traffic(wl):
         return None
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned_rank(local_rank, argv, world, port):
+    """Child of spawn_ranks: a fresh interpreter per GPU (nothing touched the GPU in the parent)."""
+    os.environ.update({"RANK": str(local_rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.argv = [sys.argv[0]] + list(argv)
+    main()
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes (spawn, so no process
+    inherits a GPU context) and wait for them; the parent never initialises the GPU."""
+    import torch.multiprocessing as mp
+    have = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if have < n:
+        raise SystemExit(f"bench.py: --gpus {n} but only {have} GPU(s) visible")
+    mp.start_processes(_spawned_rank, args=(sys.argv[1:], n, _free_port()), nprocs=n, join=True,
+                       start_method="spawn")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c5-mode", default="resident", choices=["resident", "chunked"],
                     help="c5: one graph over the resident 1 s segment, or one graph per 5 M-sample chunk")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(args.gpus)
+        return
     rank, world, local = dist_setup(args.gpus)
     device = torch.device("cuda", local)
     from gpusdr import ops
@@ -310,6 +404,7 @@ def main():
     torch.cuda.synchronize()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ops.fft_direct_blocks(local, reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -326,7 +421,8 @@ def main():
         elapsed = float(t.item())
 
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    bytes_, ops_ = chain.timed_bytes_ops()
+    direct_blocks = ops.fft_direct_blocks(local, reset=True)  # FFT blocks the accuracy guard sent to the direct form
+    bytes_, (compute_kind, ops_, peak_t) = chain.timed_bytes_ops()
     achieved_gbs = bytes_ / (kernel_ms * 1e-3) / 1e9
     achieved_t = ops_ / (kernel_ms * 1e-3) / 1e12
     total_samples = world * chain.L * args.steps
@@ -349,7 +445,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32",  # complex float32 samples; the arithmetic form is roofline.compute.kind
             "data": "synthetic (deterministic splitmix64 + tone generator, generated in HBM)",
             "config": {
                 "workload": desc,
@@ -374,19 +470,10 @@ def main():
                 "traffic": traffic,
                 "avg_launch_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": bytes_,
-                "compute": ({"kind": "f16 MFMA (2 tap limbs, fp32 accumulate)", "achieved_tflops": achieved_t,
-                             "peak_tflops": F16_PEAK_TFLOPS, "frac": achieved_t / F16_PEAK_TFLOPS,
-                             "flops_per_launch": ops_} if chain.mfma_int8 else
-                            {"kind": "f16 MFMA (2x2 limbs with per-tile scale, 3 products, fp32 accumulate)",
-                             "achieved_tflops": achieved_t, "peak_tflops": F16_PEAK_TFLOPS,
-                             "frac": achieved_t / F16_PEAK_TFLOPS, "flops_per_launch": ops_} if chain.mfma_cf else
-                            {"kind": "f16 MFMA (RF FIR, 2 tap limbs, padded Toeplitz K) + fp32 VALU (audio FIR, "
-                                     "direct form)", "achieved_tflops": achieved_t, "peak_tflops": F16_PEAK_TFLOPS,
-                             "frac": achieved_t / F16_PEAK_TFLOPS, "flops_per_launch": ops_}
-                            if isinstance(chain, AmChainRunner) else
-                            {"kind": "fp32 VALU FMA", "achieved_tflops": achieved_t,
-                             "peak_tflops": FP32_PEAK_TFLOPS, "frac": achieved_t / FP32_PEAK_TFLOPS,
-                             "flops_per_launch": ops_}),
+                "compute": {"kind": compute_kind, "achieved_tflops": achieved_t, "peak_tflops": peak_t,
+                            "frac": achieved_t / peak_t, "flops_per_launch": ops_},
+                "kernel_class": chain.kernel_class,
+                "fft_direct_blocks": direct_blocks,
             },
             "cpu_baseline": cpu,
         }

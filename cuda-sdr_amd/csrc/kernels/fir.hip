@@ -581,6 +581,11 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
   DevicePush push(device);
   if (!push.ok) return hipErrorInvalidDevice;
 
+  // long real-tap filters on cf32 / int8 IQ: FFT fast convolution (HBM-bound; fir_fft.hip)
+  if constexpr (MODE == kFirFC && (INK == kInI8IQ || INK == kInCF32) && EPI != kEpiPair) if (!mix.on) {
+    if ((kernelPolicy() & (GSDR_POLICY_NO_FFT | GSDR_POLICY_NO_MFMA)) == 0 && firFftEligible(tapCount, decimation, in, INK == kInI8IQ))
+      return launchFirFft(in, INK == kInI8IQ, taps, tapCount, decimation, out, nOut, EPI, stream);
+  }
   // int8 IQ with real taps: the exact int8 MFMA kernel when the shape allows it (the matrix-core
   // kernels take unmixed samples: a mixed stream is no longer integer)
   if constexpr (MODE == kFirFC && INK == kInI8IQ && EPI != kEpiPair) if (!mix.on) {
@@ -688,6 +693,19 @@ gsdr_amd::MixSpec mixSpec(double phase0, double radiansPerSample) {
 extern "C" {
 
 void gsdrAmdSetKernelPolicy(uint32_t flags) { gKernelPolicy.store(flags, std::memory_order_relaxed); }
+
+// Which kernel family launchFir picks for an unmixed FC FIR (same eligibility checks, same order).
+const char* gsdrAmdFirKernelClass(int int8Iq, size_t tapCount, size_t decimation, const void* input) {
+  const uint32_t pol = kernelPolicy();
+  if ((pol & (GSDR_POLICY_NO_FFT | GSDR_POLICY_NO_MFMA)) == 0 && firFftEligible(tapCount, decimation, input, int8Iq != 0))
+    return "fft";
+  if ((pol & GSDR_POLICY_NO_MFMA) == 0) {
+    if (int8Iq && firI8MfmaEligible(tapCount, decimation, input)) return "i8-mfma";
+    if (int8Iq && firI8DecMfmaEligible(tapCount, decimation, input)) return "i8-dec-mfma";
+    if (!int8Iq && firCfMfmaEligible(tapCount, decimation, input)) return "cf-mfma";
+  }
+  return "valu";
+}
 uint32_t gsdrAmdGetKernelPolicy(void) { return gKernelPolicy.load(std::memory_order_relaxed); }
 
 hipError_t gsdrFirFF(size_t decimation, const float* taps, size_t tapCount, const float* input, float* output,

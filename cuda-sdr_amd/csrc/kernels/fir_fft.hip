@@ -1,0 +1,643 @@
+// Fast-convolution (polyphase overlap-save FFT) decimating FIR for gfx950: the long-filter
+// path of gsdrFirFC / gsdrFirFCAmDemod / gsdrInt8FirFC / gsdrInt8FirFCAmDemod.
+//
+// Semantics are the reference's (src/filters/Fir.cpp:229-269; orientation pinned by
+// tests/FirTests.cpp:81-84, :196-202):  y[k] = sum_{j<T} h[j] x[kD + j].
+//
+// Algorithm:
+//   * Polyphase: with j = qD + p, y[k] = sum_p sum_q h_p[q] x_p[k + q], where
+//     x_p[m] = x[mD + p] and h_p[q] = h[qD + p] (Q = ceil(T / D) taps per phase).
+//   * Overlap-save per phase with M = 512-point FFTs: for a block of 512 rows (a row is the D
+//     consecutive samples x[mD .. mD + D - 1]), c_p[t] = sum_q h_p[q] x_p[t + q] equals the
+//     circular correlation IDFT(X_p . conj(H_p)) / M for t <= M - Q, so one block yields
+//     V = M - Q + 1 outputs (T = 1023, D = 10: Q = 103, V = 410) and the D phase spectra are
+//     summed BEFORE the single inverse FFT:  Y = sum_p X_p . G_p,  G_p = conj(DFT(h_p)) / M.
+//   * Per input sample: 5 log2(M) flops of forward FFT + 8 of spectral MAC + (5 log2 M) / D of
+//     inverse FFT, times the overlap factor M / V (~70 flops/sample at C3) - against 4 T / D =
+//     409 for the direct form: the kernel is HBM-bound, not VALU-bound.
+//   * One wave owns one block at a time: lane l holds rows l + 64 j (j = 0..7) of the block, so
+//     each phase's 512-point FFT is 8 points per lane: a radix-8 pass in registers, an 8x8
+//     digit transpose through a per-wave LDS scratch, radix-8, transpose, radix-8 (packed
+//     v_pk_* complex arithmetic). The inverse FFT runs the mirrored passes so neither direction
+//     needs a bit reversal: the spectra stay in the forward FFT's digit order (G is stored in it).
+//   * Input: coalesced 16-byte loads of the whole block (a buffer resource clipped at the input's
+//     end, so the last block reads zeros instead of faulting), transposed to rows through the
+//     same LDS scratch. int8 IQ input (the fused int8 -> cf32 -> FIR chain) carries the clamped
+//     integers x' = max(x, -127) and folds the 1/127 of gsdrInt8ToNormFloat into G.
+//   * The G table (D x 512 complex, 40 KB at D = 10) and the 512-entry twiddle table are built
+//     by each workgroup in LDS (prologue: one forward FFT per phase), so the entry points stay
+//     stateless like the reference's gsdr calls.
+//   * Epilogue: the first V outputs of the inverse FFT, AM envelope (|y|, the gsdrQuadAmDemod
+//     expression) or complex, coalesced stores.
+//
+// Accuracy: fp32 FFT round-off is relative to the block's signal level, not to each output's
+// own window (the tolerance's scale sum_j |h_j||x_kD+j|). Each block therefore measures the
+// spread of its rows' magnitudes; a block whose quietest row group is far below its loudest
+// (a burst edge, silence next to signal, inf/NaN) is recomputed in the direct fp32 form by the
+// same wave (see blockNeedsDirect and DESIGN.md 3.7 for the error model and its calibration).
+#include "kcommon.h"
+#include "fir_launch.h"
+
+#include <gsdr/gsdr.h>
+#include <gsdr/gsdr_amd.h>
+
+#include <atomic>
+#include <cmath>
+
+// Attribution builds only (tools/exp/run_fft_variants.sh); 0 in the product build.
+#ifndef GSDR_FFT_EXP
+#define GSDR_FFT_EXP 0
+#endif
+
+namespace gsdr_amd {
+namespace fftfir {
+
+// Blocks computed in the direct form by the accuracy guard since the last reset (diagnostics:
+// gsdrAmdFftDirectBlocks; one vector atomic per fallback block).
+__device__ unsigned long long gDirectBlocks;
+
+constexpr int kM = 512;       // FFT points per phase per block
+constexpr int kWaves = 8;     // waves per workgroup (one workgroup per CU)
+constexpr int kThreads = kWaves * kWave;
+constexpr int kStride = 9;    // exchange scratch row stride (complex): conflict-light b64 access
+
+enum Input : int { kCf32 = 0, kI8 = 1 };
+enum Epi : int { kComplex = 0, kAm = 1 };
+
+struct Args {
+  const void* in;
+  const float* taps;
+  void* out;
+  int64_t nOut;
+  int64_t inBytes;      // readable input bytes from `in` (loads past this return zeros)
+  int64_t nBlocks;
+  int64_t inRows;       // rows (D samples) wholly inside the input
+  int32_t T;
+  int32_t Q;            // taps per phase, ceil(T / D)
+  int32_t V;            // outputs per block
+  float inScale;        // 1 (cf32) or 1/127 (int8 IQ): folded into G
+  float guardRatio;     // direct-form fallback when max/min row-group level exceeds this
+};
+
+// ---------------------------------------------------------------- packed complex arithmetic
+// Written as VOP3P with op_sel / neg modifiers: the compiler otherwise builds the swapped /
+// negated operand with v_xor + v_mov (two extra VALU per complex product).
+__device__ __forceinline__ f2 cmul(f2 a, f2 b) {  // a * b
+  f2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+// the two halves of cmul / cmac, so independent products can be issued stage-interleaved (a
+// dependent v_pk_fma right behind the v_pk_* that writes its operand costs an s_nop on gfx950)
+__device__ __forceinline__ f2 cmul1(f2 a, f2 b) {
+  f2 t;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(b));
+  return t;
+}
+__device__ __forceinline__ f2 cmac1(f2 a, f2 b, f2 acc) {
+  f2 t;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(a), "v"(b), "v"(acc));
+  return t;
+}
+__device__ __forceinline__ f2 cmul2(f2 a, f2 b, f2 t) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+__device__ __forceinline__ f2 cmac(f2 a, f2 b, f2 acc) {  // acc + a * b
+  f2 t, r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(a), "v"(b), "v"(acc));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+__device__ __forceinline__ f2 addMi(f2 a, f2 b) {  // a - i b
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 addPi(f2 a, f2 b) {  // a + i b
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 rotM(f2 v) {  // (1 - i) v
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(v));
+  return r;
+}
+__device__ __forceinline__ f2 rotP(f2 v) {  // (1 + i) v
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// In-register 8-point DFT: z[k] <- sum_n z[n] W8^{+-nk}, W8 = exp(-2 pi i / 8) (INV: conjugate).
+template <bool INV>
+__device__ __forceinline__ void dft8(f2 (&z)[8]) {
+  constexpr float s = 0.70710678118654752440f;
+  const f2 a0 = z[0] + z[4], a1 = z[0] - z[4], a2 = z[2] + z[6], a3 = z[2] - z[6];
+  const f2 a4 = z[1] + z[5], a5 = z[1] - z[5], a6 = z[3] + z[7], a7 = z[3] - z[7];
+  const f2 b0 = a0 + a2, b2 = a0 - a2, b4 = a4 + a6, b6 = a4 - a6;
+  const f2 b1 = INV ? addPi(a1, a3) : addMi(a1, a3);
+  const f2 b3 = INV ? addMi(a1, a3) : addPi(a1, a3);
+  const f2 b5 = INV ? addPi(a5, a7) : addMi(a5, a7);
+  const f2 b7 = INV ? addMi(a5, a7) : addPi(a5, a7);
+  const f2 t5 = INV ? rotP(b5) : rotM(b5);
+  const f2 t7 = INV ? rotM(b7) : rotP(b7);
+  const f2 sv = {s, s};
+  z[0] = b0 + b4;
+  z[4] = b0 - b4;
+  z[2] = INV ? addPi(b2, b6) : addMi(b2, b6);
+  z[6] = INV ? addMi(b2, b6) : addPi(b2, b6);
+  z[1] = b1 + t5 * sv;
+  z[5] = b1 - t5 * sv;
+  z[3] = b3 - t7 * sv;
+  z[7] = b3 + t7 * sv;
+}
+
+// LDS layout (complex units): [G: D x 8 x 64][twiddles: 4 x 7 x 64][scratch: kWaves x scratch].
+// Twiddles are per-lane tables tw[s][r][l] (the four stage boundaries of the forward / inverse
+// 512-point DFT, r = 1..7), so every twiddle read is one base register + an immediate offset.
+constexpr int kTw = 4 * 7 * 64;
+struct Lds {
+  f2* g;
+  const f2* tw;  // tw + l: this lane's column
+  f2* scratch;   // this wave's
+};
+
+// Cross-lane hand-offs through the wave's own LDS scratch need no s_waitcnt between the writes
+// and the reads: one wave's DS instructions execute in issue order, so a ds_read issued after a
+// ds_write sees it (and a ds_write after a ds_read does not overtake it). Only the compiler must
+// not reorder them (it reasons per lane and would move a read above a write it proves disjoint).
+__device__ __forceinline__ void ldsOrder() { asm volatile("" ::: "memory"); }
+
+// Digit transpose of NP independent columns through the wave's scratch (NP areas of kXch
+// complex): register r of column n goes to area n at base + r * step; then every lane reads its
+// row of 8 (stride kStride). The NP columns' writes and reads are issued back to back, so one
+// column's LDS latency overlaps the other's.
+constexpr int kXch = 64 * kStride;
+template <int NP>
+__device__ __forceinline__ void exchange(f2 (&z)[NP][8], f2* s, int l, int base, int step) {
+#pragma unroll
+  for (int n = 0; n < NP; ++n)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) s[n * kXch + base + r * step] = z[n][r];
+  ldsOrder();
+#pragma unroll
+  for (int n = 0; n < NP; ++n)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) z[n][r] = s[n * kXch + l * kStride + r];
+  ldsOrder();
+}
+
+__device__ __forceinline__ f2 twiddle(const Lds& L, int stage, int r) { return L.tw[(stage * 7 + r - 1) * 64]; }
+
+template <int NP>
+__device__ __forceinline__ void loadTw(f2 (&t)[7], const Lds& L, int stage) {
+#pragma unroll
+  for (int r = 1; r < 8; ++r) t[r - 1] = twiddle(L, stage, r);
+}
+
+template <int NP>
+__device__ __forceinline__ void twiddleAll(f2 (&z)[NP][8], const f2 (&t)[7]) {
+  f2 u[NP][7];
+#pragma unroll
+  for (int n = 0; n < NP; ++n)
+#pragma unroll
+    for (int r = 1; r < 8; ++r) u[n][r - 1] = cmul1(z[n][r], t[r - 1]);
+#pragma unroll
+  for (int n = 0; n < NP; ++n)
+#pragma unroll
+    for (int r = 1; r < 8; ++r) z[n][r] = cmul2(z[n][r], t[r - 1], u[n][r - 1]);
+}
+
+// Forward 512-point DFTs of NP block columns: in: z[n][j] = x_n[l + 64 j];
+// out: lane L = 8 k0 + c, z[n][d] = X_n[k0 + 8 c + 64 d] (layout F). Each stage's twiddles are
+// loaded a stage ahead (before the exchange that precedes their use) and shared by the columns.
+template <int NP>
+__device__ __forceinline__ void fftFwd(f2 (&z)[NP][8], const Lds& L, int l) {
+  const int a = l & 7, hi = l >> 3;
+  f2 t[7];
+  loadTw<NP>(t, L, 0);  // W512^(m1 k0), m1 = l
+#pragma unroll
+  for (int n = 0; n < NP; ++n) dft8<false>(z[n]);  // over m2 -> k0
+  twiddleAll<NP>(z, t);
+  loadTw<NP>(t, L, 1);  // W64^(a c)
+  exchange<NP>(z, L.scratch, l, a * kStride + hi, 8 * kStride);  // -> lane 8 k0 + a, reg b
+#pragma unroll
+  for (int n = 0; n < NP; ++n) dft8<false>(z[n]);  // over b -> c
+  twiddleAll<NP>(z, t);
+  exchange<NP>(z, L.scratch, l, 8 * hi * kStride + a, kStride);  // -> lane 8 k0 + c, reg a
+#pragma unroll
+  for (int n = 0; n < NP; ++n) dft8<false>(z[n]);  // over a -> d
+}
+
+// Inverse (unscaled) 512-point DFT from layout F: out lane L, z[h] = y[L + 64 h].
+__device__ __forceinline__ void ifft512(f2 (&zz)[1][8], const Lds& L, int l) {
+  const int lo = l & 7, hi = l >> 3;
+  f2 t[7];
+  loadTw<1>(t, L, 2);  // W512^-((k0 + 8 c) e)
+  dft8<true>(zz[0]);   // over d -> e (lane 8 k0 + c)
+  twiddleAll<1>(zz, t);
+  loadTw<1>(t, L, 3);  // W64^-(k0 g)
+  exchange<1>(zz, L.scratch, l, 8 * hi * kStride + lo, kStride);  // -> lane 8 k0 + e, reg c
+  dft8<true>(zz[0]);   // over c -> g
+  twiddleAll<1>(zz, t);
+  exchange<1>(zz, L.scratch, l, lo * kStride + hi, 8 * kStride);  // -> lane e + 8 g, reg k0
+  dft8<true>(zz[0]);   // over k0 -> h
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t blockRsrc(const void* base, int64_t bytes) {
+  const int n = bytes <= 0 ? 0 : (bytes > 0x7fffffff ? 0x7fffffff : (int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
+}
+
+template <int D>
+constexpr int scratchComplex(int input) {
+  // two exchange areas (2 x 64 x kStride) | cf32 row-group image (64 D) | int8 block image (512 D x 2 B + 16)
+  return input == kCf32 ? (64 * D > 2 * kXch ? 64 * D : 2 * kXch)
+                        : ((1024 * D + 16) / 8 > 2 * kXch ? (1024 * D + 16 + 7) / 8 : 2 * kXch);
+}
+
+template <int D, int IN>
+constexpr size_t ldsBytes() {
+  return (size_t)(D * 8 * 64 + kTw + kWaves * scratchComplex<D>(IN)) * sizeof(f2);
+}
+
+// Prologue: the twiddle tables and G_p = inScale * conj(DFT_512(h_p)) / 512 in layout F.
+template <int D, int IN>
+__device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l) {
+  for (int n = threadIdx.x; n < kTw; n += kThreads) {
+    const int lane = n & 63, r = (n >> 6) % 7 + 1, stage = n / (7 * 64);
+    const int lo = lane & 7, hi = lane >> 3;
+    int e;  // exponent of W512 = exp(-2 pi i / 512)
+    switch (stage) {
+      case 0: e = lane * r; break;                  // forward: W512^(m1 k0)
+      case 1: e = 8 * lo * r; break;                // forward: W64^(a c)
+      case 2: e = -(hi + 8 * lo) * r; break;        // inverse: W512^-((k0 + 8 c) e)
+      default: e = -8 * hi * r; break;              // inverse: W64^-(k0 g)
+    }
+    double sn, cs;
+    sincospi(-2.0 * e / kM, &sn, &cs);
+    twAll[n] = f2{(float)cs, (float)sn};
+  }
+  __syncthreads();
+  const float sc = a.inScale / (float)kM;
+  for (int p = w; p < D; p += kWaves) {
+    f2 z[1][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int q = l + 64 * j;
+      const int t = q * D + p;
+      z[0][j] = f2{(q < a.Q && t < a.T) ? a.taps[t] : 0.0f, 0.0f};
+    }
+    fftFwd<1>(z, L, l);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) L.g[(p * 8 + d) * 64 + l] = f2{z[0][d].x * sc, -z[0][d].y * sc};
+  }
+  __syncthreads();
+}
+
+// The block's rows in registers: rows[j][p] = x[(l + 64 j) D + p] (cf32), or the raw int8 IQ
+// words of row l + 64 j (int8: D/2 dwords per row, D even).
+template <int D, int IN>
+struct Rows;
+
+template <int D>
+struct Rows<D, kCf32> {
+  f2 v[8][D];
+  __device__ __forceinline__ f2 point(int j, int p) const { return v[j][p]; }
+};
+
+template <int D>
+struct Rows<D, kI8> {
+  uint32_t v[8][D / 2];
+  // x' = max(x, -127) as float (the 1/127 lives in G)
+  __device__ __forceinline__ f2 point(int j, int p) const {
+    const uint32_t w = v[j][p >> 1];
+    const int sh = (p & 1) * 16;
+    const float re = (float)(int)(int8_t)(w >> sh);
+    const float im = (float)(int)(int8_t)(w >> (sh + 8));
+    return __builtin_elementwise_max(f2{re, im}, f2{-127.0f, -127.0f});
+  }
+};
+
+// Load block b (rows b V .. b V + 511) and transpose to rows. Loads past the input's end read 0.
+template <int D>
+__device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kCf32>& R, f2* s, int l) {
+  static_assert(D % 2 == 0, "cf32 rows: D even (whole 16-byte units per row group)");
+  const int64_t off = b * (int64_t)a.V * D * 8;  // byte offset of the block (16-byte aligned)
+  const auto rs = blockRsrc((const char*)a.in + off, a.inBytes - off);
+  // coalesced: instruction i, lane l -> 16-byte unit 64 i + l; row group j = instructions
+  // [j D/2, (j + 1) D/2)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i) {
+      const f4 u = (GSDR_FFT_EXP & 2) ? f4{(float)(l + i), (float)j, (float)(b & 7), 1.0f}
+                                      : __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((j * D / 2 + i) * 64 + l) * 16, 0, 0));
+      R.v[j][2 * i] = f2{u.x, u.y};
+      R.v[j][2 * i + 1] = f2{u.z, u.w};
+    }
+  }
+  if (GSDR_FFT_EXP & 4) return;
+  if (GSDR_FFT_EXP & 32) {
+    // rows straight from memory: lane l reads row l + 64 j (8 D bytes) as D/2 16-byte loads at a
+    // row stride (the L1 merges the instructions' partial lines); no LDS round trip
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < D / 2; ++i) {
+        const f4 u = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (l + 64 * j) * D * 8 + i * 16, 0, 0));
+        R.v[j][2 * i] = f2{u.x, u.y};
+        R.v[j][2 * i + 1] = f2{u.z, u.w};
+      }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f4* s4 = reinterpret_cast<f4*>(s);
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i) s4[i * 64 + l] = f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
+    ldsOrder();
+#pragma unroll
+    for (int p = 0; p < D; ++p) R.v[j][p] = s[l * D + p];
+    ldsOrder();
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kI8>& R, f2* s, int l) {
+  static_assert(D % 2 == 0, "int8 rows: D even (dword-aligned rows)");
+  const int64_t off = b * (int64_t)a.V * D * 2;        // byte offset of the block
+  const char* base = (const char*)a.in + off;
+  const int mis = (int)((uintptr_t)base & 15);         // 0, 4, 8 or 12 (4-byte aligned input)
+  const char* abase = base - mis;
+  // the range check is per dword: round the readable range up to whole dwords so the final
+  // 2-byte sample is not dropped with its dword (the extra <= 2 bytes share that dword, so the
+  // load stays inside the allocation's last page; they only feed rows past the input's end)
+  const auto rs = blockRsrc(abase, (a.inBytes - off + mis + 3) & ~(int64_t)3);
+  constexpr int kUnits = (1024 * D + 16) / 16;         // covers mis + 1024 D bytes
+  constexpr int kInstr = (kUnits + 63) / 64;
+  f4* s4 = reinterpret_cast<f4*>(s);
+  uint4 u[kInstr];
+#pragma unroll
+  for (int i = 0; i < kInstr; ++i) {
+    const int unit = i * 64 + l;
+    u[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, unit * 16, 0, 0));
+  }
+#pragma unroll
+  for (int i = 0; i < kInstr; ++i) {
+    const int unit = i * 64 + l;
+    if (unit < kUnits) s4[unit] = __builtin_bit_cast(f4, u[i]);
+  }
+  ldsOrder();
+  const uint32_t* s1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s) + mis);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int p = 0; p < D / 2; ++p) R.v[j][p] = s1[(l + 64 * j) * (D / 2) + p];
+  ldsOrder();
+}
+
+// Accuracy guard. The FFT's round-off is relative to the block's level; the tolerance is relative to
+// each output's own window sum_j |h_j||x_kD+j|. The block is split into segments of >= 16
+// consecutive samples (GL adjacent rows, i.e. adjacent lanes); if the loudest segment's level
+// (root of its energy sum |x|^2) exceeds guardRatio times the quietest, or the block holds inf / NaN, the
+// block is recomputed in the direct form. Rows past the input's end (the last block) are ignored.
+template <int D>
+constexpr int guardLanes() {
+  return D >= 16 ? 1 : (D >= 8 ? 2 : (D >= 4 ? 4 : 8));  // GL rows = GL * D >= 16 samples
+}
+
+template <int D, int IN>
+__device__ __forceinline__ bool blockNeedsDirect(const Args& a, const Rows<D, IN>& R, int64_t b, int l) {
+  constexpr int GL = guardLanes<D>();
+  const int64_t validRows = a.inRows - b * (int64_t)a.V;
+  float lo = INFINITY, hi = 0.0f;
+  bool nonFinite = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f2 e2 = {0.0f, 0.0f};  // segment energy sum |x|^2, one packed FMA per sample
+#pragma unroll
+    for (int p = 0; p < D; ++p) {
+      const f2 z = R.point(j, p);
+      e2 = __builtin_elementwise_fma(z, z, e2);
+    }
+    float lvl = e2.x + e2.y;
+#pragma unroll
+    for (int m = 1; m < GL; m <<= 1) lvl += __shfl_xor(lvl, m);
+    // the segment = lanes (l & ~(GL-1)) .. + GL - 1 of row group j; whole inside the input?
+    if (((l | (GL - 1)) + 64 * j) < validRows) {
+      nonFinite |= !(lvl < INFINITY);  // inf or NaN (fminf / fmaxf would drop a NaN)
+      lo = fminf(lo, lvl);
+      hi = fmaxf(hi, lvl);
+    }
+  }
+  lo = waveMinNonNeg(lo);
+  hi = waveMaxNonNeg(hi);
+  return __any(nonFinite) || !(hi <= a.guardRatio * a.guardRatio * lo);
+}
+
+// Direct-form fallback for one block (outputs b V + m, m < V): lane l computes m = l + 64 h.
+template <int D, int IN, int EPI>
+__device__ void directBlock(const Args& a, int64_t b, int l) {
+  const int64_t k0 = b * (int64_t)a.V;
+  for (int h = 0; h < 8; ++h) {
+    const int m = l + 64 * h;
+    const int64_t k = k0 + m;
+    if (m >= a.V || k >= a.nOut) continue;
+    float re = 0.0f, im = 0.0f;
+    const int64_t base = k * D;
+    for (int t = 0; t < a.T; ++t) {
+      const float hv = a.taps[t];
+      float xr, xi;
+      if (IN == kCf32) {
+        const f2 x = reinterpret_cast<const f2*>(a.in)[base + t];
+        xr = x.x;
+        xi = x.y;
+      } else {
+        const int8_t* iq = reinterpret_cast<const int8_t*>(a.in) + 2 * (base + t);
+        xr = int8ToNorm(iq[0]);
+        xi = int8ToNorm(iq[1]);
+      }
+      re = fmaf(hv, xr, re);
+      im = fmaf(hv, xi, im);
+    }
+    if (EPI == kAm)
+      reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{re, im});
+    else
+      reinterpret_cast<f2*>(a.out)[k] = f2{re, im};
+  }
+}
+
+template <int D, int IN, int EPI>
+__global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
+  extern __shared__ f2 lds[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  f2* twAll = lds + D * 8 * 64;
+  Lds L;
+  L.g = lds;
+  L.tw = twAll + l;
+  L.scratch = twAll + kTw + w * scratchComplex<D>(IN);
+  buildTables<D, IN>(a, twAll, L, w, l);
+
+  // round r: workgroup g's wave w takes block (r * groups + g) * kWaves + w, so in every round
+  // the grid streams one contiguous stretch of the input (DRAM-friendly, like a grid-stride copy)
+  // and a workgroup's waves read adjacent blocks (their overlapping rows are L2 hits)
+  const int64_t stride = (int64_t)gridDim.x * kWaves;
+  for (int64_t b = (int64_t)blockIdx.x * kWaves + w; b < a.nBlocks; b += stride) {
+    Rows<D, IN> R;
+    loadRows<D>(a, b, R, L.scratch, l);
+    if (!(GSDR_FFT_EXP & 8) && blockNeedsDirect<D, IN>(a, R, b, l)) {
+      if (l == 0) atomicAdd(&gDirectBlocks, 1ull);
+      directBlock<D, IN, EPI>(a, b, l);
+      continue;
+    }
+    constexpr int NP = (D % 2 == 0) ? 2 : 1;  // phases transformed together
+    f2 acc[1][8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) acc[0][d] = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int p = 0; p < D; p += NP) {
+      f2 z[NP][8];
+#pragma unroll
+      for (int n = 0; n < NP; ++n)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) z[n][j] = R.point(j, p + n);
+      if (!(GSDR_FFT_EXP & 1)) fftFwd<NP>(z, L, l);
+#pragma unroll
+      for (int n = 0; n < NP; ++n) {
+        f2 g[8], u[8];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) g[d] = L.g[((p + n) * 8 + d) * 64 + l];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) u[d] = cmac1(z[n][d], g[d], acc[0][d]);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) acc[0][d] = cmul2(z[n][d], g[d], u[d]);
+      }
+    }
+    if (!(GSDR_FFT_EXP & 1)) ifft512(acc, L, l);
+    const int64_t k0 = b * (int64_t)a.V;
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      const int m = l + 64 * h;
+      const int64_t k = k0 + m;
+      if (m < a.V && k < a.nOut && !((GSDR_FFT_EXP & 16) && a.T > 0)) {
+        if (EPI == kAm)
+          reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc[0][h]);
+        else
+          reinterpret_cast<f2*>(a.out)[k] = acc[0][h];
+      }
+    }
+  }
+}
+
+}  // namespace fftfir
+
+// ------------------------------------------------------------------------------------ host
+namespace {
+
+std::atomic<float> gFftGuard{8.0f};
+
+int cuCount() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    return 256;
+  return n;
+}
+
+template <int D, int IN, int EPI>
+hipError_t launchD(fftfir::Args a, hipStream_t stream) {
+  using namespace fftfir;
+  auto kernel = firFftKernel<D, IN, EPI>;
+  const size_t lds = ldsBytes<D, IN>();
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int64_t maxGroups = cuCount();
+  int64_t groups = (a.nBlocks + kWaves - 1) / kWaves;
+  if (groups > maxGroups) groups = maxGroups;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)groups), dim3(kThreads), lds, stream, a);
+  return hipGetLastError();
+}
+
+template <int IN, int EPI>
+hipError_t launchFft(fftfir::Args a, size_t D, hipStream_t stream) {
+  switch (D) {
+    case 2: return launchD<2, IN, EPI>(a, stream);
+    case 4: return launchD<4, IN, EPI>(a, stream);
+    case 6: return launchD<6, IN, EPI>(a, stream);
+    case 8: return launchD<8, IN, EPI>(a, stream);
+    case 10: return launchD<10, IN, EPI>(a, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+// Eligible: real taps (FC), D in {2,4,6,8,10}, enough taps that the FFT beats the direct forms,
+// at least 64 outputs per block, and the loads' alignment (cf32: 16-byte input; int8 IQ: 4-byte).
+bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int8Iq) {
+  const size_t D = decimation < 1 ? 1 : decimation;
+  if (!(D == 2 || D == 4 || D == 6 || D == 8 || D == 10)) return false;
+  const size_t Q = (tapCount + D - 1) / D;
+  if (tapCount < 256 || Q > (size_t)fftfir::kM - 63) return false;
+  const uintptr_t p = (uintptr_t)in;
+  return int8Iq ? (p & 3) == 0 : (p & 15) == 0;
+}
+
+hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t tapCount, size_t decimation,
+                        void* out, size_t nOut, int epi, hipStream_t stream) {
+  using namespace fftfir;
+  if (nOut == 0) return hipSuccess;
+  const size_t D = decimation < 1 ? 1 : decimation;
+  Args a{};
+  a.in = in;
+  a.taps = taps;
+  a.out = out;
+  a.nOut = (int64_t)nOut;
+  a.T = (int32_t)tapCount;
+  a.Q = (int32_t)((tapCount + D - 1) / D);
+  a.V = kM - a.Q + 1;
+  a.inBytes = (int64_t)((nOut - 1) * D + tapCount) * (int8Iq ? 2 : 8);
+  a.nBlocks = ((int64_t)nOut + a.V - 1) / a.V;
+  a.inRows = (int64_t)(((nOut - 1) * D + tapCount) / D);
+  a.inScale = int8Iq ? 1.0f / 127.0f : 1.0f;
+  a.guardRatio = gFftGuard.load(std::memory_order_relaxed);
+  const bool am = epi == kEpiAm;
+  if (int8Iq) return am ? launchFft<kI8, kAm>(a, D, stream) : launchFft<kI8, kComplex>(a, D, stream);
+  return am ? launchFft<kCf32, kAm>(a, D, stream) : launchFft<kCf32, kComplex>(a, D, stream);
+}
+
+}  // namespace gsdr_amd
+
+extern "C" {
+// Test / tuning hook (include/gsdr/gsdr_amd.h): the FFT FIR's direct-form fallback threshold on
+// the ratio of a block's loudest to quietest row level. 0 forces the direct form for every block.
+void gsdrAmdSetFftGuard(float ratio) { gsdr_amd::gFftGuard.store(ratio, std::memory_order_relaxed); }
+float gsdrAmdGetFftGuard(void) { return gsdr_amd::gFftGuard.load(std::memory_order_relaxed); }
+
+// Blocks the FFT FIR computed in the direct form since the last reset on `device` (synchronises
+// the device); reset != 0 zeroes the counter afterwards.
+hipError_t gsdrAmdFftDirectBlocks(int32_t device, uint64_t* count, int reset) {
+  int prev = 0;
+  hipError_t e = hipGetDevice(&prev);
+  if (e != hipSuccess) return e;
+  if ((e = hipSetDevice(device)) != hipSuccess) return e;
+  unsigned long long v = 0;
+  e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(gsdr_amd::fftfir::gDirectBlocks), sizeof(v));
+  if (e == hipSuccess && reset) {
+    const unsigned long long z = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(gsdr_amd::fftfir::gDirectBlocks), &z, sizeof(z));
+  }
+  if (count) *count = v;
+  (void)hipSetDevice(prev);
+  return e;
+}
+}

@@ -47,6 +47,12 @@ bool firI8DecMfmaEligible(size_t tapCount, size_t decimation, const void* in);
 hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCount, size_t decimation, void* out,
                               size_t nOut, int epi, hipStream_t stream);
 
+// cf32 (16-byte aligned) or int8 IQ (4-byte aligned) x real taps, long filters, D in {2,4,6,8,10}:
+// polyphase overlap-save FFT fast convolution (fir_fft.hip).
+bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int8Iq);
+hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t tapCount, size_t decimation,
+                        void* out, size_t nOut, int epi, hipStream_t stream);
+
 // Kernel-selection policy bits (gsdrAmdSetKernelPolicy).
 uint32_t kernelPolicy();
 

@@ -104,6 +104,13 @@ __device__ __forceinline__ float waveMinNonNeg(float v) {
   return __builtin_bit_cast(float, m);
 }
 
+// wave-wide sum of a float (butterfly over lane xor 1..32; the result in every lane)
+__device__ __forceinline__ float waveSum(float v) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
 // Four interleaved int8 IQ words (I0 Q0 I1 Q1 each) -> the clamped samples x' = max(x, -127) of

@@ -201,6 +201,7 @@ def synth_wideband_cf32(seed: int, f1: float, f2: float, first: int, n: int,
 POLICY_NO_MFMA = 1  # include/gsdr/gsdr_amd.h GSDR_POLICY_NO_MFMA
 POLICY_CF_BF16 = 2  # GSDR_POLICY_CF_BF16
 POLICY_NO_WS = 4  # GSDR_POLICY_NO_WS: barrier-synchronous decimating MFMA kernels
+POLICY_NO_FFT = 8  # GSDR_POLICY_NO_FFT: long real-tap FIRs on the direct forms, not the FFT kernel
 
 
 def set_kernel_policy(flags: int) -> int:
@@ -211,3 +212,33 @@ def set_kernel_policy(flags: int) -> int:
     prev = L.gsdrAmdGetKernelPolicy()
     L.gsdrAmdSetKernelPolicy(flags)
     return prev
+
+
+def set_fft_guard(ratio: float) -> float:
+    """FFT FIR accuracy guard (gsdrAmdSetFftGuard): blocks whose loudest row exceeds `ratio` times
+    the quietest run in the direct fp32 form; 0 forces the direct form. Returns the previous value."""
+    L = lib()
+    L.gsdrAmdGetFftGuard.restype = ctypes.c_float
+    L.gsdrAmdSetFftGuard.argtypes = [ctypes.c_float]
+    prev = L.gsdrAmdGetFftGuard()
+    L.gsdrAmdSetFftGuard(float(ratio))
+    return prev
+
+
+def fft_direct_blocks(device: int = 0, reset: bool = True) -> int:
+    """Blocks the FFT FIR sent to its direct-form fallback since the last reset (syncs the device)."""
+    L = lib()
+    L.gsdrAmdFftDirectBlocks.argtypes = [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.gsdrAmdFftDirectBlocks.restype = ctypes.c_int
+    v = ctypes.c_uint64()
+    check(L.gsdrAmdFftDirectBlocks(device, ctypes.byref(v), 1 if reset else 0), "gsdrAmdFftDirectBlocks")
+    return int(v.value)
+
+
+def fir_kernel_class(x: torch.Tensor, taps: torch.Tensor, decimation: int, int8_iq: bool = False) -> str:
+    """The kernel family the FC FIR dispatch picks for this input / shape (gsdrAmdFirKernelClass)."""
+    L = lib()
+    L.gsdrAmdFirKernelClass.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
+    L.gsdrAmdFirKernelClass.restype = ctypes.c_char_p
+    return L.gsdrAmdFirKernelClass(1 if int8_iq else 0, taps.numel(), max(1, int(decimation)),
+                                   x.data_ptr()).decode()

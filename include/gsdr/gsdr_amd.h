@@ -84,8 +84,8 @@ GSDR_API hipError_t gsdrInt8MixFirFCAmDemod(size_t decimation, const float* taps
  * Phases are reduced in double precision (n mod period) before the float trig.
  */
 /*
- * Kernel-selection policy (process-wide; default 0). GSDR_POLICY_NO_MFMA routes the int8 IQ
- * FIR through the fp32 VALU kernel instead of the exact int8 MFMA kernel (A/B comparisons).
+ * Kernel-selection policy (process-wide; default 0). GSDR_POLICY_NO_MFMA routes every FIR through
+ * the fp32 VALU direct-form kernels (no matrix-core and no FFT kernel; A/B comparisons).
  */
 #define GSDR_POLICY_NO_MFMA 1u
 /* cf32 x real taps on the bf16 x 3 split (6 products) instead of f16 x 2 with per-tile scale. */
@@ -93,8 +93,22 @@ GSDR_API hipError_t gsdrInt8MixFirFCAmDemod(size_t decimation, const float* taps
 /* Decimating MFMA FIRs on the barrier-synchronous kernels instead of the wave-specialised
  * (producer / consumer) ones. */
 #define GSDR_POLICY_NO_WS 4u
+/* Long real-tap FIRs (T >= 256, D in {2,4,6,8,10}) on the matrix-core / VALU direct forms instead of
+ * the FFT fast convolution (polyphase overlap-save, fp32). */
+#define GSDR_POLICY_NO_FFT 8u
 GSDR_API void gsdrAmdSetKernelPolicy(uint32_t flags);
+/* The kernel family the FC FIR entry points pick for this shape under the current policy:
+ * "fft", "i8-mfma", "i8-dec-mfma", "cf-mfma" or "valu" (diagnostics / benchmark labels). */
+GSDR_API const char* gsdrAmdFirKernelClass(int int8Iq, size_t tapCount, size_t decimation, const void* input);
 GSDR_API uint32_t gsdrAmdGetKernelPolicy(void);
+/* FFT FIR accuracy guard: a block whose loudest row (D consecutive samples, sum of max(|re|,|im|))
+ * exceeds `ratio` times its quietest, or that holds inf/NaN, is computed in the direct fp32 form.
+ * Default 8; 0 forces the direct form everywhere (tests). */
+GSDR_API void gsdrAmdSetFftGuard(float ratio);
+GSDR_API float gsdrAmdGetFftGuard(void);
+/* Diagnostics: blocks the FFT FIR computed in the direct form on `device` since the last reset
+ * (synchronises the device; reset != 0 zeroes the counter). */
+GSDR_API hipError_t gsdrAmdFftDirectBlocks(int32_t device, uint64_t* count, int reset);
 
 GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
                                     uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,

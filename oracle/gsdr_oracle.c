@@ -241,3 +241,53 @@ void orc_chain_fc_am_f32(size_t decimation, const float* taps, size_t tapCount, 
                          size_t numOutputs, int threads) {
   run_chain(decimation, taps, tapCount, NULL, inComplex, out, numOutputs, threads);
 }
+
+/* ---- C1 CPU baseline: real float32 FIR (CosineSource -> 63-tap FF) ----- */
+typedef struct {
+  size_t D, T, k0, k1;
+  const float* taps;
+  const float* x;
+  float* out;
+} FfJob;
+
+static void* run_ff_shard(void* arg) {
+  const FfJob* j = (const FfJob*)arg;
+  for (size_t kb = j->k0; kb < j->k1; kb += kReg) {
+    float acc[kReg];
+    const size_t nt = (j->k1 - kb) < kReg ? (j->k1 - kb) : kReg;
+    for (int i = 0; i < kReg; ++i) acc[i] = 0.0f;
+    if (nt == kReg) {
+      for (size_t q = 0; q < j->T; ++q) {
+        const float h = j->taps[q];
+        const float* xs = j->x + kb * j->D + q;
+        for (int i = 0; i < kReg; ++i) acc[i] = fmaf(h, xs[(size_t)i * j->D], acc[i]);
+      }
+    } else {
+      for (size_t i = 0; i < nt; ++i)
+        for (size_t q = 0; q < j->T; ++q) acc[i] = fmaf(j->taps[q], j->x[(kb + i) * j->D + q], acc[i]);
+    }
+    for (size_t i = 0; i < nt; ++i) j->out[kb + i] = acc[i];
+  }
+  return NULL;
+}
+
+void orc_fir_ff_f32(size_t decimation, const float* taps, size_t tapCount, const float* x, float* out,
+                    size_t numOutputs, int threads) {
+  if (numOutputs == 0 || tapCount == 0) return;
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tids[256];
+  FfJob jobs[256];
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].D = decimation == 0 ? 1 : decimation;
+    jobs[t].T = tapCount;
+    jobs[t].k0 = numOutputs * (size_t)t / (size_t)threads;
+    jobs[t].k1 = numOutputs * (size_t)(t + 1) / (size_t)threads;
+    jobs[t].taps = taps;
+    jobs[t].x = x;
+    jobs[t].out = out;
+  }
+  for (int t = 1; t < threads; ++t) pthread_create(&tids[t], NULL, run_ff_shard, &jobs[t]);
+  run_ff_shard(&jobs[0]);
+  for (int t = 1; t < threads; ++t) pthread_join(tids[t], NULL);
+}

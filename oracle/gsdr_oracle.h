@@ -62,6 +62,10 @@ void orc_chain_i8_fc_am_f32(size_t decimation, const float* taps, size_t tapCoun
 void orc_chain_fc_am_f32(size_t decimation, const float* taps, size_t tapCount, const float* inComplex, float* out,
                          size_t numOutputs, int threads);
 
+/* real f32 -> FF FIR, float32 direct form (the C1 CPU configuration). */
+void orc_fir_ff_f32(size_t decimation, const float* taps, size_t tapCount, const float* x, float* out,
+                    size_t numOutputs, int threads);
+
 void orc_multiply_cc(const float* a, const float* b, float* out, size_t n);
 void orc_quad_fm_demod_f64(const float* in, double gain, double* out, size_t nOut);
 

@@ -28,7 +28,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liborcl.so")
+_LIB_V4_PATH = os.path.join(_HERE, "_build", "liborcl_v4.so")
 _lib = None
+_baseline_lib = None
 
 SAMPLE_FLOAT_COMPLEX = 0  # SampleType.h:20-25
 SAMPLE_FLOAT = 1
@@ -41,31 +43,63 @@ def build() -> str:
     return _LIB_PATH
 
 
+def host_has_avx512() -> bool:
+    """x86-64-v4 needs avx512f/bw/dq/vl (the flags gcc's -march=x86-64-v4 assumes)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    flags = set(line.split(":", 1)[1].split())
+                    return {"avx512f", "avx512bw", "avx512dq", "avx512vl"} <= flags
+    except OSError:
+        pass
+    return False
+
+
+def baseline_isa() -> str:
+    return "x86-64-v4 (AVX-512)" if host_has_avx512() and os.path.exists(_LIB_V4_PATH) else "x86-64-v3 (AVX2+FMA)"
+
+
+def baseline_lib():
+    """The timed CPU baseline's library: the AVX-512 build when the host supports it."""
+    global _baseline_lib
+    if _baseline_lib is None:
+        if host_has_avx512() and os.path.exists(_LIB_V4_PATH):
+            _baseline_lib = _declare(ctypes.CDLL(_LIB_V4_PATH))
+        else:
+            _baseline_lib = lib()
+    return _baseline_lib
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
-        sz, vp, f32, f64, i32, u64 = (ctypes.c_size_t, ctypes.c_void_p, ctypes.c_float, ctypes.c_double,
-                                      ctypes.c_int, ctypes.c_uint64)
-        L.orc_fir_output_count.argtypes = [sz, sz, sz]
-        L.orc_fir_output_count.restype = sz
-        L.orc_fir_f64.argtypes = [i32, i32, sz, vp, sz, vp, vp, vp, sz]
-        L.orc_int8_to_norm.argtypes = [ctypes.c_int8]
-        L.orc_int8_to_norm.restype = f32
-        L.orc_int8_to_float.argtypes = [vp, vp, sz]
-        L.orc_quad_am_demod.argtypes = [vp, vp, sz]
-        L.orc_multiply_cc.argtypes = [vp, vp, vp, sz]
-        L.orc_quad_fm_demod_f64.argtypes = [vp, f64, vp, sz]
-        L.orc_cosine_f.argtypes = [f32, f32, vp, sz]
-        L.orc_cosine_c.argtypes = [f32, f32, vp, sz]
-        L.orc_synth_iq_int8.argtypes = [u64, f64, f64, f64, u64, vp, sz]
-        L.orc_synth_wideband_cf32.argtypes = [u64, f64, f64, u64, vp, sz]
-        L.orc_chain_i8_fc_am_f32.argtypes = [sz, vp, sz, vp, vp, sz, i32]
-        L.orc_chain_fc_am_f32.argtypes = [sz, vp, sz, vp, vp, sz, i32]
-        _lib = L
+        _lib = _declare(ctypes.CDLL(_LIB_PATH))
     return _lib
+
+
+def _declare(L):
+    sz, vp, f32, f64, i32, u64 = (ctypes.c_size_t, ctypes.c_void_p, ctypes.c_float, ctypes.c_double,
+                                  ctypes.c_int, ctypes.c_uint64)
+    L.orc_fir_output_count.argtypes = [sz, sz, sz]
+    L.orc_fir_output_count.restype = sz
+    L.orc_fir_f64.argtypes = [i32, i32, sz, vp, sz, vp, vp, vp, sz]
+    L.orc_int8_to_norm.argtypes = [ctypes.c_int8]
+    L.orc_int8_to_norm.restype = f32
+    L.orc_int8_to_float.argtypes = [vp, vp, sz]
+    L.orc_quad_am_demod.argtypes = [vp, vp, sz]
+    L.orc_multiply_cc.argtypes = [vp, vp, vp, sz]
+    L.orc_quad_fm_demod_f64.argtypes = [vp, f64, vp, sz]
+    L.orc_cosine_f.argtypes = [f32, f32, vp, sz]
+    L.orc_cosine_c.argtypes = [f32, f32, vp, sz]
+    L.orc_synth_iq_int8.argtypes = [u64, f64, f64, f64, u64, vp, sz]
+    L.orc_synth_wideband_cf32.argtypes = [u64, f64, f64, u64, vp, sz]
+    L.orc_chain_i8_fc_am_f32.argtypes = [sz, vp, sz, vp, vp, sz, i32]
+    L.orc_chain_fc_am_f32.argtypes = [sz, vp, sz, vp, vp, sz, i32]
+    L.orc_fir_ff_f32.argtypes = [sz, vp, sz, vp, vp, sz, i32]
+    return L
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -182,20 +216,32 @@ def synth_wideband_cf32(seed: int, f1: float, f2: float, first: int, n: int) -> 
     return out[:n]
 
 
-def chain_i8_fc_am_f32(taps, iq, decimation, n_out, threads=1) -> np.ndarray:
+def chain_i8_fc_am_f32(taps, iq, decimation, n_out, threads=1, baseline=False) -> np.ndarray:
     """CPU baseline: int8 IQ -> cf32 -> FC FIR -> AM envelope, float32 direct form."""
     t = np.ascontiguousarray(taps, dtype=np.float32)
     x = np.ascontiguousarray(iq, dtype=np.int8)
     out = np.empty(max(n_out, 1), dtype=np.float32)
-    lib().orc_chain_i8_fc_am_f32(decimation, _ptr(t), len(t), _ptr(x), _ptr(out), n_out, threads)
+    (baseline_lib() if baseline else lib()).orc_chain_i8_fc_am_f32(decimation, _ptr(t), len(t), _ptr(x), _ptr(out),
+                                                                   n_out, threads)
     return out[:n_out]
 
 
-def chain_fc_am_f32(taps, x, decimation, n_out, threads=1) -> np.ndarray:
+def chain_fc_am_f32(taps, x, decimation, n_out, threads=1, baseline=False) -> np.ndarray:
     t = np.ascontiguousarray(taps, dtype=np.float32)
     xx = np.ascontiguousarray(x, dtype=np.complex64)
     out = np.empty(max(n_out, 1), dtype=np.float32)
-    lib().orc_chain_fc_am_f32(decimation, _ptr(t), len(t), _ptr(xx), _ptr(out), n_out, threads)
+    (baseline_lib() if baseline else lib()).orc_chain_fc_am_f32(decimation, _ptr(t), len(t), _ptr(xx), _ptr(out),
+                                                                n_out, threads)
+    return out[:n_out]
+
+
+def fir_ff_f32(taps, x, decimation, n_out, threads=1, baseline=False) -> np.ndarray:
+    """C1 CPU configuration: real f32 FIR, float32 direct form, `threads` time shards."""
+    t = np.ascontiguousarray(taps, dtype=np.float32)
+    xx = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(max(n_out, 1), dtype=np.float32)
+    (baseline_lib() if baseline else lib()).orc_fir_ff_f32(decimation, _ptr(t), len(t), _ptr(xx), _ptr(out), n_out,
+                                                           threads)
     return out[:n_out]
 
 

@@ -36,6 +36,19 @@ def _host(t):
     return t.cpu().numpy()
 
 
+class _Policy:
+    """with _Policy(ops, flags): run a block under a kernel-selection policy."""
+
+    def __init__(self, ops, flags):
+        self.ops, self.flags = ops, flags
+
+    def __enter__(self):
+        self.prev = self.ops.set_kernel_policy(self.flags)
+
+    def __exit__(self, *exc):
+        self.ops.set_kernel_policy(self.prev)
+
+
 def _check_fir(y, y64, bound, what):
     err = np.abs(y.astype(np.complex128) - y64)
     assert np.all(err <= FIR_TOL * bound + 1e-30), (what, float(np.max(err / (bound + 1e-30))))
@@ -240,8 +253,9 @@ def test_int8_decimating_mfma_path(ops, orc, T, D, n_out):
     taps = orc.lowpass_taps(T, 0.4 / D).astype(np.float32)
     taps[T // 3] *= -2.0
     iq_d, taps_d = _dev(iq), _dev(taps)
-    y = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))
-    am = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=True))
+    with _Policy(ops, ops.POLICY_NO_FFT):
+        y = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))
+        am = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=True))
     x = orc.int8_to_float(iq).view(np.complex64)
     y64, bound = orc.fir_f64(taps, x, D, n_out)
     _check_fir(y, y64, bound, ("i8-dec-mfma", T, D, n_out))
@@ -268,17 +282,17 @@ def test_int8_decimating_wave_specialised_bit_exact(ops, orc, T, D, n_out, off):
     taps = orc.lowpass_taps(T, 0.4 / D).astype(np.float32)
     iq_d, taps_d = _dev(iq)[off:], _dev(taps)
     for am in (False, True):
-        y_ws = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=am))
-        prev = ops.set_kernel_policy(ops.POLICY_NO_WS)
-        try:
+        with _Policy(ops, ops.POLICY_NO_FFT):
+            y_ws = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=am))
+        with _Policy(ops, ops.POLICY_NO_WS | ops.POLICY_NO_FFT):
             y_sync = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=am))
-        finally:
-            ops.set_kernel_policy(prev)
         assert y_ws.tobytes() == y_sync.tobytes(), ("i8-ws-vs-sync", T, D, n_out, off, am)
     m = min(n_out, 5000)
     x = orc.int8_to_float(iq[off: off + 2 * ((m - 1) * D + T)]).view(np.complex64)
     y64, bound = orc.fir_f64(taps, x, D, m)
-    _check_fir(_host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))[:m], y64, bound, ("i8-ws", T, D, off))
+    with _Policy(ops, ops.POLICY_NO_FFT):
+        y_ws = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))[:m]
+    _check_fir(y_ws, y64, bound, ("i8-ws", T, D, off))
 
 
 def test_int8_decimating_mfma_misaligned(ops, orc):
@@ -288,7 +302,8 @@ def test_int8_decimating_mfma_misaligned(ops, orc):
     iq = rng.integers(-128, 128, size=2 * ((n_out - 1) * D + T) + 16).astype(np.int8)
     taps = orc.lowpass_taps(T, 0.04)
     for off in (2, 4, 6, 14):
-        y = _host(ops.fir(_dev(taps), _dev(iq)[off:], D, n_out, int8_iq=True))
+        with _Policy(ops, ops.POLICY_NO_FFT):
+            y = _host(ops.fir(_dev(taps), _dev(iq)[off:], D, n_out, int8_iq=True))
         y64, bound = orc.fir_f64(taps, orc.int8_to_float(iq[off:]).view(np.complex64), D, n_out)
         _check_fir(y, y64, bound, ("i8-dec-misaligned", off))
 
@@ -306,8 +321,9 @@ def test_cf_mfma_path(ops, orc, T, D, n_out):
     x = (rng.standard_normal(n_in) + 1j * rng.standard_normal(n_in)).astype(np.complex64)
     taps = orc.lowpass_taps(T, 0.4 / D).astype(np.float32)
     x_d, taps_d = _dev(x), _dev(taps)
-    y = _host(ops.fir(taps_d, x_d, D, n_out))
-    am = _host(ops.fir(taps_d, x_d, D, n_out, am=True))
+    with _Policy(ops, ops.POLICY_NO_FFT):
+        y = _host(ops.fir(taps_d, x_d, D, n_out))
+        am = _host(ops.fir(taps_d, x_d, D, n_out, am=True))
     y64, bound = orc.fir_f64(taps, x, D, n_out)
     _check_fir(y, y64, bound, ("cf-mfma", T, D, n_out))
     assert am.tobytes() == orc.quad_am_demod(y).tobytes()
@@ -319,9 +335,11 @@ def test_cf_mfma_path(ops, orc, T, D, n_out):
     assert np.all(np.abs(y.astype(np.complex128) - y_valu) <= 2 * FIR_TOL * bound + 1e-30)
 
 
-def test_cf_mfma_dynamic_range(ops, orc):
-    """Bursts 1e6 apart in amplitude inside one tile window: the bf16 x 3 split keeps every
-    output within 1e-6 of its OWN window's sum |h||x| (a scaled f16 split would not)."""
+@pytest.mark.parametrize("no_fft", [True, False])
+def test_cf_mfma_dynamic_range(ops, orc, no_fft):
+    """Bursts 1e6 apart in amplitude inside one tile window: the MFMA kernels keep every output
+    within 1e-6 of its OWN window's sum |h||x| (their per-tile direct path); with the FFT kernel
+    (no_fft=False) the blocks straddling a burst edge take its direct-form fallback."""
     T, D, n_out = 1023, 10, 12000
     rng = np.random.default_rng(5)
     n_in = (n_out - 1) * D + T
@@ -329,9 +347,10 @@ def test_cf_mfma_dynamic_range(ops, orc):
     amp = np.where((np.arange(n_in) // 3000) % 2 == 0, 1.0, 1e-6).astype(np.float32)
     x = (x * amp).astype(np.complex64)
     taps = orc.lowpass_taps(T, 0.04).astype(np.float32)
-    y = _host(ops.fir(_dev(taps), _dev(x), D, n_out))
+    with _Policy(ops, ops.POLICY_NO_FFT if no_fft else 0):
+        y = _host(ops.fir(_dev(taps), _dev(x), D, n_out))
     y64, bound = orc.fir_f64(taps, x, D, n_out)
-    _check_fir(y, y64, bound, "dynamic-range")
+    _check_fir(y, y64, bound, ("dynamic-range", no_fft))
 
 
 @pytest.mark.parametrize("T,D,n_out,quiet", [(1023, 10, 300_000, True), (1023, 1, 200_000, False),
@@ -348,12 +367,10 @@ def test_cf_mfma_wave_specialised_matches_sync(ops, orc, T, D, n_out, quiet):
     taps = orc.lowpass_taps(T, 0.4 / D).astype(np.float32)
     x_d, taps_d = _dev(x), _dev(taps)
     for am in (False, True):
-        y_ws = _host(ops.fir(taps_d, x_d, D, n_out, am=am))
-        prev = ops.set_kernel_policy(ops.POLICY_NO_WS)
-        try:
+        with _Policy(ops, ops.POLICY_NO_FFT):
+            y_ws = _host(ops.fir(taps_d, x_d, D, n_out, am=am))
+        with _Policy(ops, ops.POLICY_NO_WS | ops.POLICY_NO_FFT):
             y_sync = _host(ops.fir(taps_d, x_d, D, n_out, am=am))
-        finally:
-            ops.set_kernel_policy(prev)
         # identical arithmetic; only the K-padding units that the synchronous kernel also folds
         # into a tile's scale statistics may move a tile's scale (or direct decision)
         diff = y_ws != y_sync
@@ -361,7 +378,9 @@ def test_cf_mfma_wave_specialised_matches_sync(ops, orc, T, D, n_out, quiet):
         assert np.max(np.abs(y_ws - y_sync)) <= 1e-6 * np.max(np.abs(y_sync)), ("ws-vs-sync", T, D, am)
     sl = slice(0, min(n_out, 20_000))
     y64, bound = orc.fir_f64(taps, x[: (sl.stop - 1) * D + T], D, sl.stop)
-    _check_fir(_host(ops.fir(taps_d, x_d, D, n_out))[sl], y64, bound, ("ws", T, D))
+    with _Policy(ops, ops.POLICY_NO_FFT):
+        y_ws = _host(ops.fir(taps_d, x_d, D, n_out))[sl]
+    _check_fir(y_ws, y64, bound, ("ws", T, D))
 
 
 def test_cf_mfma_misaligned_falls_back(ops, orc):

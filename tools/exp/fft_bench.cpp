@@ -1,0 +1,153 @@
+// Microbenchmark of attribution builds of the FFT FIR (tools/exp/run_fft_variants.sh): C3 shape
+// (2^28 - 6 cf32 samples, 1023 taps, D = 10, AM epilogue) and the C5 RF shape (125 M int8 IQ
+// samples, 1023 taps, D = 10), HIP-event timed, every variant's output compared with the first.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define DECL(N)                                                                                        \
+  namespace f##N {                                                                                     \
+  hipError_t launchFirFft(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t); \
+  }
+VARIANT_DECLS
+
+typedef hipError_t (*LaunchFn)(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t);
+
+__global__ void fillKernel(float* x, size_t n, uint64_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const double ph = 2.0 * M_PI * fmod(0.013 * (double)(i / 2), 1.0);
+    uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 31;
+    x[i] = (float)((i & 1) ? sin(ph) : cos(ph)) + 0.01f * ((float)(int32_t)(z >> 32) * (1.0f / 2147483648.0f));
+  }
+}
+
+// reference read bandwidth: grid-stride float4 loads (optionally non-temporal), one sum per thread
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int NT>
+__global__ void streamRead(const f4v* x, size_t n4, float* sink) {
+  float acc = 0.0f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    f4v v;
+    if (NT) v = __builtin_nontemporal_load(x + i);
+    else v = x[i];
+    acc += v.x + v.y + v.z + v.w;
+  }
+  if (acc == 12345.678f) sink[0] = acc;
+}
+
+// per-wave chunked loads like the FFT kernel: each wave reads 40 KB blocks (40 x 1 KB coalesced
+// dwordx4 instructions) then consumes them; W waves per workgroup, one workgroup per CU
+template <int W, int AUX>
+__global__ void chunkRead(const char* x, size_t nBlocks, float* sink) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  float acc = 0.0f;
+  for (size_t b = blockIdx.x * (size_t)W + w; b < nBlocks; b += (size_t)gridDim.x * W) {
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + b * 40960), (short)0, 40960, 0x00020000);
+    float4 v[40];
+#pragma unroll
+    for (int i = 0; i < 40; ++i) v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (i * 64 + l) * 16, 0, AUX));
+#pragma unroll
+    for (int i = 0; i < 40; ++i) acc += v[i].x + v[i].w;
+  }
+  if (acc == 12345.678f) sink[0] = acc;
+}
+
+void readBw(void* x, size_t bytes) {
+  float* sink;
+  hipMalloc(&sink, 64);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  auto timeit = [&](const char* name, auto launch) {
+    for (int w = 0; w < 2; ++w) launch();
+    hipEventRecord(e0);
+    for (int r = 0; r < 10; ++r) launch();
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("read   %-28s %9.1f us  %7.3f TB/s\n", name, ms * 100.0, bytes / (ms * 1e-4) / 1e12);
+    fflush(stdout);
+  };
+  const size_t n4 = bytes / 16;
+  for (int bpc : {2, 4, 8}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "grid-stride f4 x%d/CU", bpc);
+    timeit(nm, [&] { streamRead<0><<<256 * bpc, 256>>>((const f4v*)x, n4, sink); });
+    snprintf(nm, sizeof nm, "grid-stride f4 nt x%d/CU", bpc);
+    timeit(nm, [&] { streamRead<1><<<256 * bpc, 256>>>((const f4v*)x, n4, sink); });
+  }
+  const size_t nb = bytes / 40960;
+  timeit("chunk 8 waves", [&] { chunkRead<8, 0><<<256, 512>>>((const char*)x, nb, sink); });
+  timeit("chunk 8 waves nt", [&] { chunkRead<8, 2><<<256, 512>>>((const char*)x, nb, sink); });
+  timeit("chunk 4 waves", [&] { chunkRead<4, 0><<<256, 256>>>((const char*)x, nb, sink); });
+  timeit("chunk 16 waves", [&] { chunkRead<16, 0><<<256, 1024>>>((const char*)x, nb, sink); });
+  hipFree(sink);
+}
+
+int main() {
+  struct Shape { const char* name; size_t n, T, D; bool i8; } shapes[] = {{"c3", (1u << 28) - 6, 1023, 10, false},
+                                                                          {"c5rf", 125000000, 1023, 10, true}};
+  struct V { const char* name; LaunchFn fn; } vars[] = {VARIANT_TABLE};
+  const int nv = sizeof(vars) / sizeof(vars[0]);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (auto& sh : shapes) {
+    const size_t nOut = (sh.n - sh.T) / sh.D + 1, nIn = (nOut - 1) * sh.D + sh.T;
+    void *x, *out, *ref;
+    float* taps;
+    const size_t inBytes = nIn * (sh.i8 ? 2 : 8);
+    hipMalloc(&x, inBytes + 64);
+    hipMalloc(&taps, sh.T * 4);
+    hipMalloc(&out, nOut * 4);
+    hipMalloc(&ref, nOut * 4);
+    if (sh.i8) {
+      std::vector<int8_t> h(inBytes);
+      for (size_t i = 0; i < inBytes; ++i) h[i] = (int8_t)(100.0 * cos(0.37 * (double)i) + (double)((i * 7919) % 7) - 3);
+      hipMemcpy(x, h.data(), inBytes, hipMemcpyHostToDevice);
+    } else {
+      fillKernel<<<1024, 256>>>((float*)x, 2 * nIn, 12345);
+    }
+    std::vector<float> ht(sh.T);
+    for (size_t j = 0; j < sh.T; ++j) {
+      const double n = (double)j - (sh.T - 1) / 2.0;
+      ht[j] = (float)(0.08 * (n == 0 ? 1.0 : sin(M_PI * 0.08 * n) / (M_PI * 0.08 * n)) *
+                      (0.42 - 0.5 * cos(2 * M_PI * j / (sh.T - 1)) + 0.08 * cos(4 * M_PI * j / (sh.T - 1))));
+    }
+    hipMemcpy(taps, ht.data(), sh.T * 4, hipMemcpyHostToDevice);
+    if (!sh.i8) readBw(x, inBytes);
+    std::vector<float> a(nOut), b(nOut);
+    for (int v = 0; v < nv; ++v) {
+      void* o = v == 0 ? ref : out;
+      for (int w = 0; w < 3; ++w) vars[v].fn(x, sh.i8, taps, sh.T, sh.D, o, nOut, 2, 0);
+      const int reps = 20;
+      hipEventRecord(e0);
+      for (int r = 0; r < reps; ++r) vars[v].fn(x, sh.i8, taps, sh.T, sh.D, o, nOut, 2, 0);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      double md = 0;
+      if (v > 0) {
+        hipMemcpy(a.data(), ref, nOut * 4, hipMemcpyDeviceToHost);
+        hipMemcpy(b.data(), out, nOut * 4, hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < nOut; ++i) md = fmax(md, fabs((double)a[i] - (double)b[i]));
+      }
+      const double us = ms * 1e3 / reps;
+      printf("%-6s %-16s %9.1f us/launch  %7.3f TB/s algorithmic  max|diff| vs base %.3g\n", sh.name, vars[v].name, us,
+             (double)(inBytes + nOut * 4) / (us * 1e-6) / 1e12, md);
+      fflush(stdout);
+    }
+    hipFree(x);
+    hipFree(taps);
+    hipFree(out);
+    hipFree(ref);
+  }
+  return 0;
+}

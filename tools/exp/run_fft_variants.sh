@@ -1,0 +1,39 @@
+#!/bin/bash
+# Build (here) and run (on the GPU box) attribution variants of csrc/kernels/fir_fft.hip.
+#   bash tools/exp/run_fft_variants.sh build   # CPU container
+#   bash tools/exp/run_fft_variants.sh run     # GPU box
+# GSDR_FFT_EXP bits: 1 no FFT math, 2 no global loads, 4 no LDS transposition, 8 no guard,
+# 16 no stores.
+set -eu
+cd "$(dirname "$0")/../.."
+OUT=tools/exp/_build_fft
+KSRC=cuda-sdr_amd/csrc/kernels/fir_fft.hip
+VARIANTS=${VARIANTS:-"base|
+nofft|-DGSDR_FFT_EXP=1
+noload|-DGSDR_FFT_EXP=2
+notrans|-DGSDR_FFT_EXP=4
+noguard|-DGSDR_FFT_EXP=8
+nostore|-DGSDR_FFT_EXP=16
+fft_only|-DGSDR_FFT_EXP=30
+rowload|-DGSDR_FFT_EXP=32
+rowload_only|-DGSDR_FFT_EXP=57
+rowload_nofft|-DGSDR_FFT_EXP=33
+load_only|-DGSDR_FFT_EXP=29"}
+if [ "${1:-build}" = build ]; then
+  mkdir -p $OUT
+  decls=""; table=""; objs=""; i=0
+  while IFS='|' read -r name flags; do
+    [ -z "$name" ] && continue
+    hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Iinclude -Icuda-sdr_amd/csrc/kernels \
+      -Dgsdr_amd=f$i -DgsdrAmdSetFftGuard=f${i}_sg -DgsdrAmdGetFftGuard=f${i}_gg -DgsdrAmdFftDirectBlocks=f${i}_db \
+      $flags -c $KSRC -o $OUT/f$i.o &
+    decls="$decls DECL($i)"; table="$table {\"$name\", f$i::launchFirFft},"; objs="$objs $OUT/f$i.o"
+    i=$((i+1))
+  done <<< "$VARIANTS"
+  wait
+  hipcc --offload-arch=gfx950 -O2 -std=c++20 "-DVARIANT_DECLS=$decls" "-DVARIANT_TABLE=$table" -c tools/exp/fft_bench.cpp -o $OUT/main.o
+  hipcc --offload-arch=gfx950 $OUT/main.o $objs -o $OUT/fft_bench
+  echo built $OUT/fft_bench
+else
+  timeout -k 10 300 $OUT/fft_bench
+fi
