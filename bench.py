@@ -146,13 +146,16 @@ class ShardedChain:
         g = self.geom
         if ev is not None:
             ev[0].record()
-        if self.kind == "i8":
+        # the fused carry writes the unconsumed tail (T - D samples); with D = 1 that is the whole
+        # T - 1 halo in front of the segment
+        fused_carry = self.kind == "i8" and self.D == 1
+        if fused_carry:
             self.ops.fir_am_i8_carry(self.taps, self.buf, self.D, g.outputs, self.out, self.ring.halo)
         else:
             self._fir(self.buf, g.outputs, self.out)
         if ev is not None:
             ev[1].record()
-        if self.kind != "i8":
+        if not fused_carry:
             self.ring.halo.copy_(self.ring.tail)
 
     @property

@@ -31,6 +31,8 @@
 // sample pair, and the taps are scaled by a block-uniform 2^sc and split into two f16 limbs as in
 // fir_i8_mfma.hip: 2 v_mfma_f32_32x32x16_f16 per K-step instead of 6 bf16 products.
 #include <algorithm>
+#include <atomic>
+#include <cstddef>
 #include <mutex>
 
 #include "kcommon.h"
@@ -71,6 +73,8 @@ struct CfFirArgs {
   int32_t padShift;   // plane unit u lives at u + (u >> padShift)
   int32_t planeStride;  // bytes between the six planes (limb l, component c at 2 l + c)
   int32_t dbp;          // wave-specialised kernels: two partial-sum buffers
+  int32_t spinLimit;    // wave-specialised kernels: s_sleep iterations before a wait gives up
+  uint32_t* abortOut;   // wave-specialised kernels: host-visible abort counter (wsAbortWord)
 };
 
 __device__ __forceinline__ int cfPhys(int u, int p) { return u + (u >> p); }
@@ -652,7 +656,7 @@ constexpr int kWsProducers = 4;
 constexpr int kWsPThreads = kWsProducers * kWave;           // 256
 constexpr int kWsThreads = kCfThreads + kWsPThreads;        // 768
 constexpr int kWsDirect = 0x7fffffff;                       // plane-set mode: direct fp32 tile
-constexpr int kWsSpinLimit = 1 << 22;                       // s_sleep(1) iterations (~0.1 s)
+constexpr int kWsSpinLimit = 1 << 22;                       // default s_sleep(1) iterations (~0.1 s)
 
 struct WsCtl {
   int planesFull[2];
@@ -664,7 +668,11 @@ struct WsCtl {
   int abort;
   int mode[2];                        // per plane set: scale exponent sx, or kWsDirect
   float stat[2][2][kWsProducers];     // [tile parity][max, smallest block max][producer wave]
+  // set once by thread 0 (not part of the zeroed hand-off words above)
+  int spinLimit;
+  uint32_t* abortOut;
 };
+constexpr int kWsCtlZeroWords = (int)(offsetof(WsCtl, spinLimit) / 4);
 
 __device__ __forceinline__ void wsSignal(int* p, int lane) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS writes/reads complete
@@ -684,8 +692,12 @@ __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
     const int v = waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (v >= target) break;
     if (waveUniform(__hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
-    if (it > kWsSpinLimit) {
+    if (it > c->spinLimit) {
+      // a hand-off that never completes: release every other wait so the grid drains, and count
+      // the failure where the host sees it (the entry points report it as hipErrorLaunchTimeOut)
       __hip_atomic_store(&c->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if ((threadIdx.x & (kWave - 1)) == 0 && c->abortOut != nullptr)
+        __hip_atomic_fetch_add(c->abortOut, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -1033,7 +1045,11 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
 #endif
 
   // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), block max; zero both plane sets --------
-  if (tid < (int)(sizeof(WsCtl) / 4)) reinterpret_cast<int*>(c)[tid] = 0;
+  if (tid < kWsCtlZeroWords) reinterpret_cast<int*>(c)[tid] = 0;
+  if (tid == 0) {
+    c->spinLimit = a.spinLimit;
+    c->abortOut = a.abortOut;
+  }
   const int off0 = 31 * D;
   const int span = off0 + 128 * KS;
   float hm = 0.0f;
@@ -1100,6 +1116,8 @@ struct I8DecArgs {
   int32_t padShift;
   int32_t planeStride;  // bytes between the I and Q f16 planes
   int32_t dbp;          // wave-specialised kernel: two partial-sum buffers
+  int32_t spinLimit;    // as CfFirArgs
+  uint32_t* abortOut;
 };
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -1348,7 +1366,11 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
   if (n <= 0) return;
 
   // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), block max; zero both plane sets --------
-  if (tid < (int)(sizeof(WsCtl) / 4)) reinterpret_cast<int*>(c)[tid] = 0;
+  if (tid < kWsCtlZeroWords) reinterpret_cast<int*>(c)[tid] = 0;
+  if (tid == 0) {
+    c->spinLimit = a8.spinLimit;
+    c->abortOut = a8.abortOut;
+  }
   const int off0 = 31 * D;
   const int span = off0 + 128 * KS;
   float hm = 0.0f;
@@ -1609,6 +1631,62 @@ hipError_t launchI8DecKS(const I8DecArgs& a, size_t lds, int grid, int epi, hipS
   }
 }
 
+// Wave-specialised kernels: a wait that gives up (a hand-off that never completes) leaves that
+// launch's outputs undefined. The aborting waves count it in a pinned, device-mapped host word per
+// device; the next launch of a wave-specialised kernel on that device reports it as
+// hipErrorLaunchTimeOut, and gsdrAmdWsAborts reads it after a device synchronisation.
+constexpr int kMaxDevices = 64;
+std::mutex gAbortMu;
+uint32_t* gAbortHost[kMaxDevices];
+uint32_t* gAbortDev[kMaxDevices];
+std::atomic<int> gWsSpinLimit{kWsSpinLimit};
+
+// Device view of this device's abort word (allocated on first use; nullptr if that fails).
+uint32_t* wsAbortWord(int dev) {
+  if (dev < 0 || dev >= kMaxDevices) return nullptr;
+  std::lock_guard<std::mutex> lock(gAbortMu);
+  if (gAbortDev[dev] == nullptr) {
+    // not a stream operation: allowed even if the caller's stream is being captured
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+      *static_cast<volatile uint32_t*>(h) = 0;
+      if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) {
+        gAbortHost[dev] = static_cast<uint32_t*>(h);
+        gAbortDev[dev] = static_cast<uint32_t*>(d);
+      } else {
+        (void)hipHostFree(h);
+      }
+    }
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+  }
+  return gAbortDev[dev];
+}
+
+// Aborts counted since the last read on `dev` (host read of the mapped word; clears it).
+uint32_t takeWsAborts(int dev) {
+  if (dev < 0 || dev >= kMaxDevices) return 0;
+  uint32_t* h;
+  {
+    std::lock_guard<std::mutex> lock(gAbortMu);
+    h = gAbortHost[dev];
+  }
+  return h == nullptr ? 0u : __atomic_exchange_n(h, 0u, __ATOMIC_SEQ_CST);
+}
+
+// Before a wave-specialised launch: report an earlier launch's abort, and arm this one.
+hipError_t wsPrepare(int32_t& spinLimit, uint32_t*& abortOut) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (takeWsAborts(dev) != 0) return hipErrorLaunchTimeOut;
+  spinLimit = gWsSpinLimit.load(std::memory_order_relaxed);
+  abortOut = wsAbortWord(dev);
+  return hipSuccess;
+}
+
 }  // namespace
 
 // Attribution builds (tools/exp/cf_bench): copy out and clear the wave-specialised kernel's stamps.
@@ -1677,7 +1755,10 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
       size_t lds = 8 * (size_t)a.planeStride + 2 * kCfPartialBytes;
       a.dbp = lds <= (size_t)kCfDynLdsMax;  // double-buffered partials when they fit
       if (!a.dbp) lds -= kCfPartialBytes;
-      if (lds <= (size_t)kCfDynLdsMax) return launchCfWsAny(a, Wl, lds, grid, epi, stream);
+      if (lds <= (size_t)kCfDynLdsMax) {
+        if (hipError_t e = wsPrepare(a.spinLimit, a.abortOut); e != hipSuccess) return e;
+        return launchCfWsAny(a, Wl, lds, grid, epi, stream);
+      }
     }
   }
   static std::mutex mu;
@@ -1760,7 +1841,10 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
       size_t lds = 4 * (size_t)a.planeStride + 2 * kCfPartialBytes;
       a.dbp = lds <= (size_t)kCfDynLdsMax;
       if (!a.dbp) lds -= kCfPartialBytes;
-      if (lds <= (size_t)kCfDynLdsMax) return launchI8WsAny(a, Wl, lds, grid, epi, stream);
+      if (lds <= (size_t)kCfDynLdsMax) {
+        if (hipError_t e = wsPrepare(a.spinLimit, a.abortOut); e != hipSuccess) return e;
+        return launchI8WsAny(a, Wl, lds, grid, epi, stream);
+      }
     }
   }
   static std::mutex mu;
@@ -1794,3 +1878,32 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
 }
 
 }  // namespace gsdr_amd
+
+extern "C" {
+// include/gsdr/gsdr_amd.h: wave-specialised kernel hand-off limit and abort diagnostics.
+void gsdrAmdSetWsSpinLimit(int32_t iterations) {
+  gsdr_amd::gWsSpinLimit.store(iterations < 0 ? 0 : iterations, std::memory_order_relaxed);
+}
+int32_t gsdrAmdGetWsSpinLimit(void) { return gsdr_amd::gWsSpinLimit.load(std::memory_order_relaxed); }
+
+hipError_t gsdrAmdWsAborts(int32_t device, uint64_t* count, int reset) {
+  int prev = 0;
+  hipError_t e = hipGetDevice(&prev);
+  if (e != hipSuccess) return e;
+  if ((e = hipSetDevice(device)) != hipSuccess) return e;
+  e = hipDeviceSynchronize();
+  uint64_t v = 0;
+  if (e == hipSuccess) {
+    if (reset) {
+      v = gsdr_amd::takeWsAborts(device);
+    } else {
+      std::lock_guard<std::mutex> lock(gsdr_amd::gAbortMu);
+      const uint32_t* h = device >= 0 && device < gsdr_amd::kMaxDevices ? gsdr_amd::gAbortHost[device] : nullptr;
+      v = h ? __atomic_load_n(h, __ATOMIC_SEQ_CST) : 0;
+    }
+  }
+  if (count) *count = v;
+  (void)hipSetDevice(prev);
+  return e;
+}
+}

@@ -448,22 +448,30 @@ __device__ void directBlock(const Args& a, int64_t b, int l) {
     const int m = l + 64 * h;
     const int64_t k = k0 + m;
     if (m >= a.V || k >= a.nOut) continue;
+    // blocked sums (64 taps per partial, then added to the running total), as the other direct
+    // forms: a plain 1023-term chain can exceed the 1e-6 sum|h||x| tolerance
     float re = 0.0f, im = 0.0f;
     const int64_t base = k * D;
-    for (int t = 0; t < a.T; ++t) {
-      const float hv = a.taps[t];
-      float xr, xi;
-      if (IN == kCf32) {
-        const f2 x = reinterpret_cast<const f2*>(a.in)[base + t];
-        xr = x.x;
-        xi = x.y;
-      } else {
-        const int8_t* iq = reinterpret_cast<const int8_t*>(a.in) + 2 * (base + t);
-        xr = int8ToNorm(iq[0]);
-        xi = int8ToNorm(iq[1]);
+    for (int t0 = 0; t0 < a.T; t0 += 64) {
+      const int t1 = t0 + 64 < a.T ? t0 + 64 : a.T;
+      float pr = 0.0f, pi = 0.0f;
+      for (int t = t0; t < t1; ++t) {
+        const float hv = a.taps[t];
+        float xr, xi;
+        if (IN == kCf32) {
+          const f2 x = reinterpret_cast<const f2*>(a.in)[base + t];
+          xr = x.x;
+          xi = x.y;
+        } else {
+          const int8_t* iq = reinterpret_cast<const int8_t*>(a.in) + 2 * (base + t);
+          xr = int8ToNorm(iq[0]);
+          xi = int8ToNorm(iq[1]);
+        }
+        pr = fmaf(hv, xr, pr);
+        pi = fmaf(hv, xi, pi);
       }
-      re = fmaf(hv, xr, re);
-      im = fmaf(hv, xi, im);
+      re += pr;
+      im += pi;
     }
     if (EPI == kAm)
       reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{re, im});
@@ -588,7 +596,12 @@ bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int
   const size_t Q = (tapCount + D - 1) / D;
   if (tapCount < 256 || Q > (size_t)fftfir::kM - 63) return false;
   const uintptr_t p = (uintptr_t)in;
-  return int8Iq ? (p & 3) == 0 : (p & 15) == 0;
+  // int8 IQ: the exact f16 MFMA kernels are faster where they apply (C5 RF stage, 125 M samples:
+  // 195 us wave-specialised MFMA vs 263 us FFT); the FFT takes the shapes they cannot
+  if (int8Iq)
+    return (p & 3) == 0 && ((kernelPolicy() & GSDR_POLICY_PREFER_FFT) != 0 ||
+                            (!firI8MfmaEligible(tapCount, decimation, in) && !firI8DecMfmaEligible(tapCount, decimation, in)));
+  return (p & 15) == 0;
 }
 
 hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t tapCount, size_t decimation,

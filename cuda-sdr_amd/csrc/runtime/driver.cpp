@@ -2,6 +2,8 @@
 // differences from the reference.
 #include "driver.h"
 
+#include "buffers.h"
+
 #include <gpusdrpipeline/abi/errors.h>
 
 #include <algorithm>
@@ -211,30 +213,81 @@ Status SteppingDriver::doSourceOutput(Source* source) {
       if (mPortBuffers[p] == nullptr) mPortBuffers[p] = r.value;
     }
   }
+  // Fan-out: readOutput fills the port's first buffer and the driver copies it into the other
+  // sinks' buffers, so the first buffer is capped (a view of the same memory) to the least room
+  // any sink of the port lent; a sink that lent more simply receives fewer bytes this step.
+  for (size_t p = 0; p < nPorts; ++p) {
+    if (si.ports[p].size() < 2) continue;
+    size_t firstRef = 0;
+    for (size_t q = 0; q < p; ++q) firstRef += si.ports[q].size();
+    size_t room = SIZE_MAX;
+    for (size_t s = 0; s < si.ports[p].size(); ++s)
+      room = std::min(room, mBufferRefs[firstRef + s]->range()->remaining());
+    IBuffer* first = mBufferRefs[firstRef].get();
+    if (first->range()->remaining() > room) {
+      Ref<IBufferRangeMutableCapacity> range = new (std::nothrow) BufferRange();
+      Ref<IBuffer> view = range.get() ? new (std::nothrow) BufferSlice(first, 0, range.get()) : nullptr;
+      Status vs = view.get() ? Status_Success : Status_OutOfMemory;
+      if (vs == Status_Success) {
+        range->setCapacity(first->range()->endOffset() + room);
+        vs = range->setUsedRange(first->range()->offset(), first->range()->endOffset());
+      }
+      if (vs != Status_Success) {
+        cancel(mBufferRefs.size());
+        return vs;
+      }
+      mPortBuffers[p] = view.get();
+      mViewRefs.emplace_back(std::move(view));
+    }
+  }
   Status st = source->readOutput(mPortBuffers.data(), nPorts);
   if (st != Status_Success) {
     gsloge("Source [%s] readOutput failed [%u]", nameOf(source), (unsigned)st);
     cancel(mBufferRefs.size());
+    mViewRefs.clear();
     return st;
   }
+  // copy to the other sinks of each port; on any failure every checkout is cancelled (committing
+  // 0 bytes), so no sink stays checked out
   size_t ref = 0;
+  std::vector<size_t> portBytes(nPorts, 0);
   for (size_t p = 0; p < nPorts; ++p) {
     IBuffer* populated = mPortBuffers[p];
     const size_t bytes = populated->range()->used();
+    portBytes[p] = bytes;
     ++ref;  // the populated buffer
     for (size_t s = 1; s < si.ports[p].size(); ++s, ++ref) {
       IBuffer* target = mBufferRefs[ref].get();
       IBufferCopier* copier = source->getOutputCopier(p);
+      Status cs = Status_Success;
       if (copier == nullptr) {
         gsloge("Source [%s] port [%zu] feeds %zu sinks but has no output copier", nameOf(source), p,
                si.ports[p].size());
-        return Status_InvalidState;
+        cs = Status_InvalidState;
+      } else if (target->range()->remaining() < bytes) {
+        cs = Status_OutOfRange;  // unreachable: the first buffer was capped to the least room
+      } else {
+        cs = copier->copy(target->writePtr(), populated->readPtr(), bytes);
+        if (cs == Status_Success) cs = target->range()->increaseEndOffset(bytes);
       }
-      if (target->range()->remaining() < bytes) return Status_OutOfRange;
-      FWD_IF_ERR(copier->copy(target->writePtr(), populated->readPtr(), bytes));
-      FWD_IF_ERR(target->range()->increaseEndOffset(bytes));
+      if (cs != Status_Success) {
+        cancel(mBufferRefs.size());
+        mViewRefs.clear();
+        return cs;
+      }
     }
-    for (const SinkPortKey& k : si.ports[p]) FWD_IF_ERR(k.sink->commitBuffer(k.port, bytes));
+  }
+  mViewRefs.clear();
+  Status firstErr = Status_Success;
+  for (size_t p = 0; p < nPorts; ++p)
+    for (const SinkPortKey& k : si.ports[p]) {
+      // every sink commits (or cancels) even after an earlier commit failed
+      const Status cs = k.sink->commitBuffer(k.port, firstErr == Status_Success ? portBytes[p] : 0);
+      if (firstErr == Status_Success && cs != Status_Success) firstErr = cs;
+    }
+  if (firstErr != Status_Success) {
+    mBufferRefs.clear();
+    return firstErr;
   }
   mBufferRefs.clear();
   return Status_Success;

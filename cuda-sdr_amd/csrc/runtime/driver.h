@@ -80,6 +80,7 @@ class SteppingDriver final : public ISteppingDriver {
   // per-step scratch, kept to avoid reallocation on every doSourceOutput
   std::vector<Ref<IBuffer>> mBufferRefs;
   std::vector<IBuffer*> mPortBuffers;
+  std::vector<Ref<IBuffer>> mViewRefs;  // capped fan-out views (doSourceOutput)
 
   REF_COUNTED(SteppingDriver);
 };

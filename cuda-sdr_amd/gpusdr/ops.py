@@ -202,6 +202,7 @@ POLICY_NO_MFMA = 1  # include/gsdr/gsdr_amd.h GSDR_POLICY_NO_MFMA
 POLICY_CF_BF16 = 2  # GSDR_POLICY_CF_BF16
 POLICY_NO_WS = 4  # GSDR_POLICY_NO_WS: barrier-synchronous decimating MFMA kernels
 POLICY_NO_FFT = 8  # GSDR_POLICY_NO_FFT: long real-tap FIRs on the direct forms, not the FFT kernel
+POLICY_PREFER_FFT = 16  # GSDR_POLICY_PREFER_FFT: int8 IQ on the FFT kernel even where int8 MFMA applies
 
 
 def set_kernel_policy(flags: int) -> int:
@@ -242,3 +243,25 @@ def fir_kernel_class(x: torch.Tensor, taps: torch.Tensor, decimation: int, int8_
     L.gsdrAmdFirKernelClass.restype = ctypes.c_char_p
     return L.gsdrAmdFirKernelClass(1 if int8_iq else 0, taps.numel(), max(1, int(decimation)),
                                    x.data_ptr()).decode()
+
+
+def set_ws_spin_limit(iterations: int) -> int:
+    """Hand-off wait limit of the wave-specialised MFMA kernels (gsdrAmdSetWsSpinLimit, s_sleep
+    polls); returns the previous value."""
+    L = lib()
+    L.gsdrAmdGetWsSpinLimit.restype = ctypes.c_int32
+    L.gsdrAmdSetWsSpinLimit.argtypes = [ctypes.c_int32]
+    prev = L.gsdrAmdGetWsSpinLimit()
+    L.gsdrAmdSetWsSpinLimit(int(iterations))
+    return prev
+
+
+def ws_aborts(device: int = 0, reset: bool = True) -> int:
+    """Wave-specialised launches whose hand-off waits gave up since the last reset (gsdrAmdWsAborts;
+    synchronises the device). Such launches' outputs are undefined."""
+    L = lib()
+    L.gsdrAmdWsAborts.argtypes = [ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.gsdrAmdWsAborts.restype = ctypes.c_int
+    v = ctypes.c_uint64()
+    check(L.gsdrAmdWsAborts(device, ctypes.byref(v), 1 if reset else 0), "gsdrAmdWsAborts")
+    return int(v.value)

@@ -96,6 +96,9 @@ GSDR_API hipError_t gsdrInt8MixFirFCAmDemod(size_t decimation, const float* taps
 /* Long real-tap FIRs (T >= 256, D in {2,4,6,8,10}) on the matrix-core / VALU direct forms instead of
  * the FFT fast convolution (polyphase overlap-save, fp32). */
 #define GSDR_POLICY_NO_FFT 8u
+/* int8 IQ input takes the FFT fast convolution even where the int8 MFMA kernels apply (by default
+ * they do: faster for int8 at the C5 shape); A/B comparisons and tests of the int8 FFT path. */
+#define GSDR_POLICY_PREFER_FFT 16u
 GSDR_API void gsdrAmdSetKernelPolicy(uint32_t flags);
 /* The kernel family the FC FIR entry points pick for this shape under the current policy:
  * "fft", "i8-mfma", "i8-dec-mfma", "cf-mfma" or "valu" (diagnostics / benchmark labels). */
@@ -109,6 +112,15 @@ GSDR_API float gsdrAmdGetFftGuard(void);
 /* Diagnostics: blocks the FFT FIR computed in the direct form on `device` since the last reset
  * (synchronises the device; reset != 0 zeroes the counter). */
 GSDR_API hipError_t gsdrAmdFftDirectBlocks(int32_t device, uint64_t* count, int reset);
+/* Wave-specialised (producer / consumer) MFMA FIR kernels: every hand-off wait gives up after
+ * `iterations` s_sleep(1) polls (default 1 << 22, ~0.1 s), releases all other waits so the grid
+ * drains, and counts the abort in a host-visible word. Such a launch's outputs are undefined; the
+ * next gsdr* call that launches a wave-specialised kernel on that device returns
+ * hipErrorLaunchTimeOut (and clears the count). gsdrAmdWsAborts synchronises `device` and reads
+ * the count (reset != 0 clears it). */
+GSDR_API void gsdrAmdSetWsSpinLimit(int32_t iterations);
+GSDR_API int32_t gsdrAmdGetWsSpinLimit(void);
+GSDR_API hipError_t gsdrAmdWsAborts(int32_t device, uint64_t* count, int reset);
 
 GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
                                     uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,

@@ -82,7 +82,7 @@ class CounterSource final : public Source {
   CounterSource(int32_t total, size_t alignment, int32_t start = 0) : mTotal(total), mNext(start), mAlign(alignment) {}
   size_t getOutputDataSize(size_t) noexcept final { return 4 * (size_t)(mTotal - mNext); }
   size_t getOutputSizeAlignment(size_t) noexcept final { return mAlign; }
-  IBufferCopier* getOutputCopier(size_t) noexcept final { return F()->getSysMemCopier(); }
+  IBufferCopier* getOutputCopier(size_t) noexcept final { return noCopier ? nullptr : F()->getSysMemCopier(); }
   Status readOutput(IBuffer** outs, size_t n) noexcept final {
     if (n != mPorts) return Status_InvalidArgument;
     ++reads;
@@ -96,6 +96,7 @@ class CounterSource final : public Source {
   }
   void setPorts(size_t n) { mPorts = n; }
   int reads = 0;
+  bool noCopier = false;
 
  private:
   const int32_t mTotal;
@@ -256,6 +257,43 @@ void fanOut() {
   CHECK(s1->mIn.pending == x);
   CHECK(s2->mIn.pending == x);
   CHECK(src->reads == (1000 + 15) / 16);  // one readOutput per step serves both sinks
+}
+
+void fanOutUnequalBuffers() {
+  // fan-out to sinks that lend different amounts: readOutput writes only what the smallest lent
+  // buffer can take (the first buffer is capped), so no step fails with OutOfRange
+  Ref<CounterSource> src = new CounterSource(1000, 4);
+  Ref<Collect> s1 = new Collect(256), s2 = new Collect(24);  // host buffers: 256 and 64 bytes
+  Ref<ISteppingDriver> d = newDriver();
+  THROW_IF_ERR(d->connect(src.get(), 0, s1.get(), 0));
+  THROW_IF_ERR(d->connect(src.get(), 0, s2.get(), 0));
+  run(d.get(), [&] { return s1->mIn.pending.size() + s2->mIn.pending.size(); });
+  std::vector<int32_t> x(1000);
+  std::iota(x.begin(), x.end(), 0);
+  CHECK(s1->mIn.pending == x);
+  CHECK(s2->mIn.pending == x);
+  CHECK(src->reads == (1000 + 15) / 16);  // 64 bytes (the smaller lent buffer) per step
+}
+
+void fanOutErrorCancels() {
+  // a failure after the checkouts (no output copier for a fan-out port) cancels every lent
+  // buffer: no sink stays checked out, and the same sinks can lend again afterwards
+  Ref<CounterSource> src = new CounterSource(100, 4);
+  src->noCopier = true;
+  Ref<Collect> s1 = new Collect(16), s2 = new Collect(16);
+  Ref<ISteppingDriver> d = newDriver();
+  THROW_IF_ERR(d->connect(src.get(), 0, s1.get(), 0));
+  THROW_IF_ERR(d->connect(src.get(), 0, s2.get(), 0));
+  CHECK(d->doFilter() == Status_InvalidState);
+  CHECK(s1->mIn.lent == nullptr && s2->mIn.lent == nullptr);
+  CHECK(s1->mIn.pending.empty() && s2->mIn.pending.empty());
+  src->noCopier = false;
+  run(d.get(), [&] { return s1->mIn.pending.size() + s2->mIn.pending.size(); });
+  // the failed step's samples (one 64-byte buffer) were already read from the source and are
+  // dropped with it; everything after arrives at both sinks
+  std::vector<int32_t> rest(84);
+  std::iota(rest.begin(), rest.end(), 16);
+  CHECK(s1->mIn.pending == rest && s2->mIn.pending == rest);
 }
 
 void twoInputs() {
@@ -489,6 +527,8 @@ int main() {
   runCase("linear_chain", linearChain);
   runCase("alignment", alignment);
   runCase("fan_out", fanOut);
+  runCase("fan_out_unequal_buffers", fanOutUnequalBuffers);
+  runCase("fan_out_error_cancels", fanOutErrorCancels);
   runCase("two_inputs", twoInputs);
   runCase("connect_rules_and_names", connectRulesAndNames);
   runCase("exhausted_source", exhaustedSource);

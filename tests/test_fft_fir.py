@@ -76,8 +76,10 @@ def test_fft_fir_matches_float64(ops, orc, kind, T, D, n_out):
     i8 = kind == "i8"
     x_d, taps_d = _dev(x), _dev(taps)
     ops.fft_direct_blocks(reset=True)
-    y = _host(ops.fir(taps_d, x_d, D, n_out, int8_iq=i8))
-    am = _host(ops.fir(taps_d, x_d, D, n_out, int8_iq=i8, am=True))
+    with _Policy(ops, ops.POLICY_PREFER_FFT):  # int8: the FFT even where the int8 MFMA kernels apply
+        assert ops.fir_kernel_class(x_d, taps_d, D, int8_iq=i8) == "fft"
+        y = _host(ops.fir(taps_d, x_d, D, n_out, int8_iq=i8))
+        am = _host(ops.fir(taps_d, x_d, D, n_out, int8_iq=i8, am=True))
     direct = ops.fft_direct_blocks(reset=True)
     xc = orc.int8_to_float(x).view(np.complex64) if i8 else x
     y64, bound = orc.fir_f64(taps, xc, D, n_out)
@@ -194,7 +196,8 @@ def test_fft_fir_int8_alignment(ops, orc, off):
     iq = _signal("i8", n_in + 8, 2, orc)
     x_d = _dev(iq)[off:]
     taps = orc.lowpass_taps(T, 0.04, "blackman")
-    y = _host(ops.fir(_dev(taps), x_d, D, n_out, int8_iq=True))
+    with _Policy(ops, ops.POLICY_PREFER_FFT):
+        y = _host(ops.fir(_dev(taps), x_d, D, n_out, int8_iq=True))
     xc = orc.int8_to_float(iq[off:]).view(np.complex64)
     y64, bound = orc.fir_f64(taps, xc, D, n_out)
     _check(y, y64, bound, ("i8-align", off))

@@ -383,6 +383,36 @@ def test_cf_mfma_wave_specialised_matches_sync(ops, orc, T, D, n_out, quiet):
     _check_fir(y_ws, y64, bound, ("ws", T, D))
 
 
+def test_ws_abort_is_reported(ops, orc):
+    """A wave-specialised launch whose producer / consumer hand-off waits give up is not silent:
+    with the spin limit at 0 every wait that is not already satisfied aborts, the launch drains and
+    counts it in the host-visible word (gsdrAmdWsAborts), and the next wave-specialised launch on
+    the device reports hipErrorLaunchTimeOut instead of returning. After the report the count is
+    clear and a normal launch is correct again."""
+    from gpusdr._native import HipError
+    T, D, n_out = 1023, 10, 100_000
+    n_in = (n_out - 1) * D + T
+    x = orc.synth_wideband_cf32(0xAB, 0.013, 0.31, 0, n_in)
+    taps = orc.lowpass_taps(T, 0.04, "blackman")
+    x_d, taps_d = _dev(x), _dev(taps)
+    with _Policy(ops, ops.POLICY_NO_FFT):
+        assert ops.fir_kernel_class(x_d, taps_d, D) == "cf-mfma"
+        assert ops.ws_aborts(reset=True) == 0
+        prev = ops.set_ws_spin_limit(0)
+        try:
+            ops.fir(taps_d, x_d, D, n_out)
+            assert ops.ws_aborts(reset=False) > 0
+        finally:
+            ops.set_ws_spin_limit(prev)
+        with pytest.raises(HipError, match="gsdrFirFC"):
+            ops.fir(taps_d, x_d, D, n_out)
+        assert ops.ws_aborts(reset=False) == 0
+        y = _host(ops.fir(taps_d, x_d, D, n_out))
+        assert ops.ws_aborts(reset=True) == 0
+    y64, bound = orc.fir_f64(taps, x, D, n_out)
+    _check_fir(y, y64, bound, "after-abort")
+
+
 def test_cf_mfma_misaligned_falls_back(ops, orc):
     T, D, n_out = 255, 4, 3000
     rng = np.random.default_rng(9)
@@ -423,6 +453,31 @@ def test_fir_carry_streaming(ops, orc, T, L, mfma):
     y64, bound = orc.fir_f64(taps, x, 1, nblk * L)
     assert np.all(np.abs(am - np.abs(y64)) <= FIR_TOL * bound + 1e-30), (T, L, mfma)
     assert _host(buf[: 2 * H]).tobytes() == stream[len(stream) - 2 * H:].tobytes()
+
+
+@pytest.mark.parametrize("T,D,n1,n2", [(1023, 10, 5000, 7000), (255, 4, 333, 1000), (64, 3, 100, 50)])
+def test_fir_carry_decimating(ops, orc, T, D, n1, n2):
+    """gsdrInt8FirFCAmDemodCarry with D > 1: the carry is the unconsumed tail of the call's input,
+    samples [n1 D, (n1 - 1) D + T) (T - D of them). Put directly in front of the stream's next
+    samples it makes two chained calls equal one call over the whole stream."""
+    import torch
+    rng = np.random.default_rng(T + D)
+    n_in1 = (n1 - 1) * D + T
+    n_all = (n1 + n2 - 1) * D + T
+    stream = rng.integers(-128, 128, size=2 * n_all).astype(np.int8)
+    taps_d = _dev(orc.lowpass_taps(T, 0.4 / D).astype(np.float32))
+    out1 = torch.empty(n1, dtype=torch.float32, device="cuda")
+    buf = torch.zeros(2 * (n_all - n1 * D), dtype=torch.int8, device="cuda")  # [carry | rest]
+    ops.fir_am_i8_carry(taps_d, _dev(stream[: 2 * n_in1]), D, n1, out1, buf[: 2 * (T - D)])
+    buf[2 * (T - D):] = _dev(stream[2 * n_in1:])
+    # the reference count rule floor((N - (T - 1)) / D) (Fir.cpp:178-186) yields n2 - 1 here for D > 1
+    n2 = ops.fir_output_count(buf.numel() // 2, T, D)
+    out2 = torch.empty(n2, dtype=torch.float32, device="cuda")
+    ops.fir_am_i8_carry(taps_d, buf, D, n2, out2, torch.empty(2 * (T - D), dtype=torch.int8, device="cuda"))
+    chained = np.concatenate([_host(out1), _host(out2)])
+    x = orc.int8_to_float(stream).view(np.complex64)
+    y64, bound = orc.fir_f64(_host(taps_d), x, D, n1 + n2)  # one FIR over the whole stream
+    assert np.all(np.abs(chained - np.abs(y64)) <= FIR_TOL * bound + 1e-30), (T, D)
 
 
 def test_cosine_sources(ops, orc):
