@@ -48,6 +48,9 @@
 #ifndef GSDR_FFT_EXP
 #define GSDR_FFT_EXP 0
 #endif
+#ifndef GSDR_FFT_STAGGER
+#define GSDR_FFT_STAGGER 1  // s_sleep(127) rounds before waves 4-7 start (~64 x 127 cycles each)
+#endif
 
 namespace gsdr_amd {
 namespace fftfir {
@@ -414,7 +417,10 @@ constexpr int guardLanes() {
 template <int D, int IN>
 __device__ __forceinline__ bool blockNeedsDirect(const Args& a, const Rows<D, IN>& R, int64_t b, int l) {
   constexpr int GL = guardLanes<D>();
-  const int64_t validRows = a.inRows - b * (int64_t)a.V;
+  // rows of this block inside the input, as a 32-bit wave-uniform bound (lane math stays 32-bit:
+  // no 64-bit per-lane constants for the compiler to keep live across the block loop)
+  const int64_t vr64 = a.inRows - b * (int64_t)a.V;
+  const int validRows = __builtin_amdgcn_readfirstlane((int)(vr64 < kM ? vr64 : kM));
   float lo = INFINITY, hi = 0.0f;
   bool nonFinite = false;
 #pragma unroll
@@ -444,14 +450,15 @@ __device__ __forceinline__ bool blockNeedsDirect(const Args& a, const Rows<D, IN
 template <int D, int IN, int EPI>
 __device__ void directBlock(const Args& a, int64_t b, int l) {
   const int64_t k0 = b * (int64_t)a.V;
+  const int64_t left = a.nOut - k0;
+  const int nv = __builtin_amdgcn_readfirstlane((int)(left < a.V ? left : a.V));  // outputs of this block
+  const int64_t base = k0 * D;  // the block's first input sample (scalar)
   for (int h = 0; h < 8; ++h) {
     const int m = l + 64 * h;
-    const int64_t k = k0 + m;
-    if (m >= a.V || k >= a.nOut) continue;
+    if (m >= nv) continue;
     // blocked sums (64 taps per partial, then added to the running total), as the other direct
     // forms: a plain 1023-term chain can exceed the 1e-6 sum|h||x| tolerance
     float re = 0.0f, im = 0.0f;
-    const int64_t base = k * D;
     for (int t0 = 0; t0 < a.T; t0 += 64) {
       const int t1 = t0 + 64 < a.T ? t0 + 64 : a.T;
       float pr = 0.0f, pi = 0.0f;
@@ -459,11 +466,11 @@ __device__ void directBlock(const Args& a, int64_t b, int l) {
         const float hv = a.taps[t];
         float xr, xi;
         if (IN == kCf32) {
-          const f2 x = reinterpret_cast<const f2*>(a.in)[base + t];
+          const f2 x = (reinterpret_cast<const f2*>(a.in) + base)[m * D + t];
           xr = x.x;
           xi = x.y;
         } else {
-          const int8_t* iq = reinterpret_cast<const int8_t*>(a.in) + 2 * (base + t);
+          const int8_t* iq = reinterpret_cast<const int8_t*>(a.in) + 2 * base + 2 * (m * D + t);
           xr = int8ToNorm(iq[0]);
           xi = int8ToNorm(iq[1]);
         }
@@ -474,9 +481,9 @@ __device__ void directBlock(const Args& a, int64_t b, int l) {
       im += pi;
     }
     if (EPI == kAm)
-      reinterpret_cast<float*>(a.out)[k] = amEnvelope(f2{re, im});
+      (reinterpret_cast<float*>(a.out) + k0)[m] = amEnvelope(f2{re, im});
     else
-      reinterpret_cast<f2*>(a.out)[k] = f2{re, im};
+      (reinterpret_cast<f2*>(a.out) + k0)[m] = f2{re, im};
   }
 }
 
@@ -490,6 +497,13 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   L.tw = twAll + l;
   L.scratch = twAll + kTw + w * scratchComplex<D>(IN);
   buildTables<D, IN>(a, twAll, L, w, l);
+  if (w >= kWaves / 2) {
+    // stagger: the second-dispatched half of the waves (one per SIMD) starts ~4 us later, so the
+    // two waves of each SIMD run out of phase - one loading its block while the other computes -
+    // instead of all eight loading, then all computing (C3: 675 -> 591 us per launch,
+    // tools/exp/run_fft_variants.sh; larger delays resynchronise and do not help)
+    for (int i = 0; i < GSDR_FFT_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+  }
 
   // round r: workgroup g's wave w takes block (r * groups + g) * kWaves + w, so in every round
   // the grid streams one contiguous stretch of the input (DRAM-friendly, like a grid-stride copy)

@@ -11,6 +11,9 @@
 #define DECL(N)                                                                                        \
   namespace f##N {                                                                                     \
   hipError_t launchFirFft(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t); \
+  uint32_t kernelPolicy() { return 0; }                                                              \
+  bool firI8MfmaEligible(size_t, size_t, const void*) { return false; }                              \
+  bool firI8DecMfmaEligible(size_t, size_t, const void*) { return false; }                           \
   }
 VARIANT_DECLS
 
