@@ -75,26 +75,46 @@ def lowpass(num_taps, cutoff, window):
     return (h / h.sum()).astype(np.float32)
 
 
-def dist_setup(n_gpus):
+def dist_setup(n_gpus, backend="nccl", share_gpu=False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n_gpus:
         raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}; launch one rank per GPU "
                          "(torch.distributed.run) or let bench.py spawn them (WORLD_SIZE unset)")
+    dev_index = 0 if share_gpu else local
+    torch.cuda.set_device(dev_index)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    return rank, world, local
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, dev_index
+
+
+# Each step streams at least this many bytes through distinct buffers, so a step's working set never
+# sits in the 256 MiB Infinity Cache (MI355X_MICROARCH.md: FETCH_SIZE counts MALL hits; C2's one
+# second of signal is only 120 MB): the input / output buffer sets rotate step by step.
+MALL_BYTES = 256 << 20
+
+
+class _Slot:
+    """One [halo | segment] input buffer, its output, and its halo ring."""
+
+    def __init__(self, g, w, dt, device, ring_cls, stage, incoming):
+        H, L = g.halo, g.seg_len
+        self.buf = torch.zeros(w * (H + L), dtype=dt, device=device)
+        self.seg = self.buf[w * H:]
+        self.ring = ring_cls(g, self.buf[: w * H], self.seg[w * (L - H):], incoming, stage)
+        self.bulk_x = self.seg[w * g.bulk_input_offset():]
+        self.out = torch.empty(g.outputs, dtype=torch.float32, device=device)
 
 
 class ShardedChain:
     """Per-rank state of one time-sharded FIR -> AM step (gpusdr/shard.py protocol)."""
 
-    def __init__(self, ops, wl, rank, world, device):
+    def __init__(self, ops, wl, rank, world, device, stage=False):
         from gpusdr.shard import HaloRing, ShardGeometry
         desc, kind, L, T, D, cutoff, window, fs = WORKLOADS[wl]
         self.ops, self.kind, self.L, self.T, self.D = ops, kind, L, T, D
@@ -103,17 +123,25 @@ class ShardedChain:
         self.taps = torch.from_numpy(lowpass(T, cutoff, window)).to(device)
         w = 2 if kind == "i8" else 1  # tensor elements per sample (int8 I,Q | complex64)
         dt = torch.int8 if kind == "i8" else torch.complex64
-        self.buf = torch.zeros(w * (H + L), dtype=dt, device=device)  # [halo | segment]
-        self.seg = self.buf[w * H:]
-        if kind == "i8":
-            ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, g.segment_start(0), L, out=self.seg)
-        else:
-            ops.synth_wideband_cf32(0xC3, 0.013, 0.31, g.segment_start(0), L, out=self.seg)
+        step_bytes = (H + L) * (2 if kind == "i8" else 8) + g.outputs * 4
+        self.n_slots = max(1, -(-int(1.5 * MALL_BYTES) // step_bytes))
         incoming = torch.zeros(w * H, dtype=dt, device=device) if (world > 1 and rank == 0) else None
-        self.ring = HaloRing(g, self.buf[: w * H], self.seg[w * (L - H):], incoming)
-        self.bulk_x = self.seg[w * g.bulk_input_offset():]
-        self.out = torch.empty(g.outputs, dtype=torch.float32, device=device)
+        self.slots = [_Slot(g, w, dt, device, HaloRing, stage, incoming) for _ in range(self.n_slots)]
+        for k, sl in enumerate(self.slots):  # slot k holds the stream position of step k
+            if kind == "i8":
+                ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, g.segment_start(k), L, out=sl.seg)
+            else:
+                ops.synth_wideband_cf32(0xC3, 0.013, 0.31, g.segment_start(k), L, out=sl.seg)
+        self.cur = 0
         self.ev = None
+
+    @property
+    def slot(self):
+        return self.slots[self.cur]
+
+    @property
+    def buf(self):
+        return self.slot.buf
 
     def _fir(self, x, n_out, out):
         if n_out > 0:
@@ -127,40 +155,44 @@ class ShardedChain:
 
     def bulk(self):
         """Outputs [head, L/D): inputs entirely inside this rank's segment (the timed kernel)."""
-        g = self.geom
+        g, sl = self.geom, self.slot
         if self.ev is not None:
             self.ev[0].record()
-        self._fir(self.bulk_x, g.outputs - g.head_outputs, self.out[g.head_outputs:])
+        self._fir(sl.bulk_x, g.outputs - g.head_outputs, sl.out[g.head_outputs:])
         if self.ev is not None:
             self.ev[1].record()
 
     def head(self):
         """Outputs [0, head): read the halo in front of the segment."""
-        self._fir(self.buf, self.geom.head_outputs, self.out[: self.geom.head_outputs])
+        sl = self.slot
+        self._fir(sl.buf, self.geom.head_outputs, sl.out[: self.geom.head_outputs])
 
     def step(self, ev=None):
         self.ev = ev
+        g, sl = self.geom, self.slot
+        nxt = self.slots[(self.cur + 1) % self.n_slots]
         if not self.single:
-            self.ring.step(self.bulk, self.head)
-            return
-        g = self.geom
-        if ev is not None:
-            ev[0].record()
-        # the fused carry writes the unconsumed tail (T - D samples); with D = 1 that is the whole
-        # T - 1 halo in front of the segment
-        fused_carry = self.kind == "i8" and self.D == 1
-        if fused_carry:
-            self.ops.fir_am_i8_carry(self.taps, self.buf, self.D, g.outputs, self.out, self.ring.halo)
+            sl.ring.step(self.bulk, self.head)
+            if self.n_slots > 1 and g.rank == 0:
+                nxt.ring.halo.copy_(sl.ring.halo)  # the halo that arrived for the next step
         else:
-            self._fir(self.buf, g.outputs, self.out)
-        if ev is not None:
-            ev[1].record()
-        if not fused_carry:
-            self.ring.halo.copy_(self.ring.tail)
+            if ev is not None:
+                ev[0].record()
+            # the fused carry writes the unconsumed tail (T - D samples); with D = 1 that is the
+            # whole T - 1 halo in front of the next step's segment
+            if self.kind == "i8" and self.D == 1:
+                self.ops.fir_am_i8_carry(self.taps, sl.buf, self.D, g.outputs, sl.out, nxt.ring.halo)
+            else:
+                self._fir(sl.buf, g.outputs, sl.out)
+            if ev is not None:
+                ev[1].record()
+            if not (self.kind == "i8" and self.D == 1):
+                nxt.ring.halo.copy_(sl.ring.tail)
+        self.cur = (self.cur + 1) % self.n_slots
 
     @property
     def kernel_class(self):
-        x = self.buf if self.single else self.bulk_x
+        x = self.slot.buf if self.single else self.slot.bulk_x
         return self.ops.fir_kernel_class(x, self.taps, self.D, int8_iq=(self.kind == "i8"))
 
     def timed_bytes_ops(self):
@@ -171,6 +203,53 @@ class ShardedChain:
         n_in = (n - 1) * self.D + self.T
         in_bytes = n_in * (2 if self.kind == "i8" else 8)
         return in_bytes + n * 4, kernel_compute(self.kernel_class, n, self.T, self.D)
+
+
+class AmChainSharded:
+    """C5 default: the time-sharded AM receive chain (gpusdr.shard.AmChainShard) - every rank runs
+    int8 IQ -> 1023-tap FIR, D = 10 -> AM -> 255-tap audio FIR, D = 20 over [cascaded halo |
+    segment], the halo ((Ta - 1) D + T - 1 -> 3 600 samples) coming from the previous rank over the
+    ring (its own previous step at N = 1). Input slots rotate past the Infinity Cache."""
+
+    def __init__(self, ops, rank, world, device, stage=False):
+        from gpusdr.shard import AmChainShard, ChainShardGeometry
+        desc, kind, L, T, D, cutoff, window, fs = WORKLOADS["c5"]
+        Ta, Da, cut_a, win_a = C5_AUDIO
+        self.ops, self.kind, self.L, self.T, self.D, self.Ta, self.Da = ops, kind, L, T, D, Ta, Da
+        self.mode = "sharded"
+        self.geom = g = ChainShardGeometry(rank, world, L, T, D, Ta, Da)
+        rf = torch.from_numpy(lowpass(T, cutoff, window)).to(device)
+        au = torch.from_numpy(lowpass(Ta, cut_a, win_a)).to(device)
+        self.rf_taps = rf
+        step_bytes = 2 * (g.halo + L) + 4 * g.rf_outputs + 4 * g.outputs
+        self.n_slots = max(1, -(-int(1.5 * MALL_BYTES) // step_bytes))
+        self.slots = [AmChainShard(g, rf, au, device, stage) for _ in range(self.n_slots)]
+        for k, sh in enumerate(self.slots):
+            ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, g.segment_start(k), L, out=sh.seg)
+        self.cur = 0
+        self.single = world == 1
+        self.kernel_class = ops.fir_kernel_class(self.slots[0].seg, rf, D, int8_iq=True)
+
+    def step(self, ev=None):
+        g, sh = self.geom, self.slots[self.cur]
+        nxt = self.slots[(self.cur + 1) % self.n_slots]
+        if ev is not None:
+            ev[0].record()
+        sh.step()
+        if ev is not None:
+            ev[1].record()
+        if self.n_slots > 1 and (g.world == 1 or g.rank == 0):
+            nxt.ring.halo.copy_(sh.ring.halo)
+        self.cur = (self.cur + 1) % self.n_slots
+
+    def timed_bytes_ops(self):
+        """Per step (the timed region is the whole step: RF FIR + AM bulk and head, audio FIR):
+        int8 input (segment + halo) read once + audio written once; RF kernel arithmetic plus the
+        audio FIR's direct-form flops."""
+        g = self.geom
+        kind, fl, peak = kernel_compute(self.kernel_class, g.rf_outputs, self.T, self.D)
+        return 2 * (g.halo + self.L) + 4 * g.outputs, (f"RF: {kind}; audio FIR: fp32 VALU direct form",
+                                                       fl + g.outputs * self.Ta * 2, peak)
 
 
 def kernel_compute(cls, n_out, T, D):
@@ -335,6 +414,11 @@ def cpu_baseline(wl, seconds_target=8.0):
 
 
 def kernel_name(chain):
+    if isinstance(chain, AmChainSharded):
+        body = {"fft": "firFftKernel", "i8-dec-mfma": "firI8WsKernel", "valu": "firLdsKernel"}.get(
+            chain.kernel_class, chain.kernel_class)
+        return (f"whole C5 step: gsdrInt8FirFCAmDemod ({body}) bulk + head, gsdrFirFF audio "
+                "(firSmallKernel); HIP events around the step")
     if isinstance(chain, AmChainRunner):
         return (f"gsdrAmChain {chain.mode} step graph (RF FIR+AM, audio FIR, history copies; "
                 "HIP events around the whole step)")
@@ -371,13 +455,14 @@ def _spawned_rank(local_rank, argv, world, port):
     main()
 
 
-def spawn_ranks(n):
+def spawn_ranks(n, share_gpu=False):
     """`bench.py --gpus N` without a launcher: start N fresh rank processes (spawn, so no process
     inherits a GPU context) and wait for them; the parent never initialises the GPU."""
     import torch.multiprocessing as mp
     have = torch.cuda.device_count()  # does not initialise the GPU on this image
-    if have < n:
-        raise SystemExit(f"bench.py: --gpus {n} but only {have} GPU(s) visible")
+    if have < n and not share_gpu:
+        raise SystemExit(f"bench.py: --gpus {n} but only {have} GPU(s) visible "
+                         "(--share-gpu --backend gloo runs the ranks on one GPU, for testing)")
     mp.start_processes(_spawned_rank, args=(sys.argv[1:], n, _free_port()), nprocs=n, join=True,
                        start_method="spawn")
 
@@ -389,18 +474,31 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--c5-mode", default="resident", choices=["resident", "chunked"],
-                    help="c5: one graph over the resident 1 s segment, or one graph per 5 M-sample chunk")
+    ap.add_argument("--c5-mode", default="sharded", choices=["sharded", "resident", "chunked"],
+                    help="c5: the time-sharded chain with its cascaded halo (default); or the gsdrAmChain "
+                         "executor: one graph over the resident 1 s segment / one graph per 5 M-sample chunk "
+                         "(N = 1 semantics: at N > 1 those run replicas)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for the halo ring (nccl = RCCL over xGMI; gloo stages "
+                         "halos through host memory)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="run every rank on cuda:0 (testing the multi-rank path on a one-GPU box; gloo)")
     args = ap.parse_args()
+    if args.share_gpu and args.backend != "gloo":
+        raise SystemExit("bench.py: --share-gpu needs --backend gloo (RCCL runs one rank per GPU)")
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        spawn_ranks(args.gpus)
+        spawn_ranks(args.gpus, args.share_gpu)
         return
-    rank, world, local = dist_setup(args.gpus)
+    rank, world, local = dist_setup(args.gpus, args.backend, args.share_gpu)
     device = torch.device("cuda", local)
+    stage = args.backend != "nccl"
     from gpusdr import ops
-    chain = AmChainRunner(ops, rank, world, device, args.c5_mode) if args.workload == "c5" else \
-        ShardedChain(ops, args.workload, rank, world, device)
+    if args.workload == "c5":
+        chain = (AmChainSharded(ops, rank, world, device, stage) if args.c5_mode == "sharded" else
+                 AmChainRunner(ops, rank, world, device, args.c5_mode))
+    else:
+        chain = ShardedChain(ops, args.workload, rank, world, device, stage)
 
     for _ in range(args.warmup):
         chain.step()
@@ -419,7 +517,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -448,7 +546,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",  # complex float32 samples; the arithmetic form is roofline.compute.kind
+            "dtype": "f32",  # complex float32 samples / fp32 accumulation; the arithmetic form:
+            "arithmetic": compute_kind,
             "data": "synthetic (deterministic splitmix64 + tone generator, generated in HBM)",
             "config": {
                 "workload": desc,
@@ -458,10 +557,13 @@ def main():
                 "input": "int8 IQ" if chain.kind == "i8" else "cf32",
                 "parallelism": ("disjoint time ranges per rank, history primed by warm-up (no collective)"
                                 if chain.geom is None else
-                                f"time-shard x{world} (ring halo of {chain.geom.halo} samples over RCCL)")
-                if world > 1 else "single GPU (halo = own history carry)",
-                **({"c5_mode": chain.mode, "chunk_samples": C5_CHUNK, "audio_taps": chain.Ta,
-                    "audio_decimation": chain.Da} if isinstance(chain, AmChainRunner) else {}),
+                                f"time-shard x{world} (ring halo of {chain.geom.halo} samples over "
+                                f"{'RCCL' if args.backend == 'nccl' else args.backend + ', host-staged'}"
+                                f"{', ranks sharing cuda:0' if args.share_gpu else ''})")
+                if world > 1 else f"single GPU (halo = own history carry, {chain.geom.halo if chain.geom else 0} samples)",
+                "buffer_sets": getattr(chain, "n_slots", 1),
+                **({"c5_mode": chain.mode, "audio_taps": chain.Ta, "audio_decimation": chain.Da}
+                   if args.workload == "c5" else {}),
             },
             "roofline": {
                 "bound": "hbm",

@@ -74,18 +74,113 @@ class ShardGeometry:
         return (self.rank - 1) % self.world
 
 
+@dataclass(frozen=True)
+class ChainShardGeometry:
+    """The cascaded halo of the AM receive chain (C5: int8 IQ -> FC FIR (T, D) -> AM -> FF FIR
+    (Ta, Da)), SURVEY.md 8(e): an audio output needs Ta - 1 earlier AM samples, each of which needs
+    T - 1 earlier inputs, so a segment needs (Ta - 1) D + T - 1 input samples in front of it
+    (3 562 at T = 1023, D = 10, Ta = 255), rounded up here to a multiple of D Da so the decimation
+    phases of both FIRs are kept (3 600).
+
+    Each rank runs the chain afresh over [halo | segment] every step: RF outputs k (inputs
+    [kD, kD + T) of that window) -> AM -> audio outputs; that yields exactly L / (D Da) audio
+    samples, the padded stream's outputs from index segment_start / (D Da) on (the stream fed
+    `halo` zeros first, as ShardGeometry feeds T - 1 zeros). The RF outputs whose windows start
+    in the segment (k >= halo / D) need no halo: the bulk launch runs while the exchange is in
+    flight; the head_rf outputs before them read the halo."""
+    rank: int
+    world: int
+    seg_len: int
+    taps: int
+    decimation: int
+    audio_taps: int
+    audio_decimation: int
+
+    def __post_init__(self):
+        if self.seg_len % (self.decimation * self.audio_decimation) != 0:
+            raise ValueError("segment length must be a multiple of D * Da")
+        if self.seg_len < self.halo:
+            raise ValueError("segment shorter than the halo")
+        if self.outputs_of(self.halo + self.seg_len) != self.outputs:
+            raise AssertionError("halo does not yield exactly L / (D Da) audio samples")
+
+    @property
+    def halo(self) -> int:
+        need = (self.audio_taps - 1) * self.decimation + self.taps - 1
+        unit = self.decimation * self.audio_decimation
+        return -(-need // unit) * unit
+
+    def rf_outputs_of(self, n_in: int) -> int:
+        return max(0, (n_in - (self.taps - 1)) // self.decimation)  # Fir.cpp:178-186
+
+    def outputs_of(self, n_in: int) -> int:
+        return max(0, (self.rf_outputs_of(n_in) - (self.audio_taps - 1)) // self.audio_decimation)
+
+    @property
+    def rf_outputs(self) -> int:
+        return self.rf_outputs_of(self.halo + self.seg_len)
+
+    @property
+    def head_rf(self) -> int:
+        """RF outputs whose input windows start in the halo."""
+        return self.halo // self.decimation
+
+    @property
+    def outputs(self) -> int:
+        return self.seg_len // (self.decimation * self.audio_decimation)
+
+    def segment_start(self, step: int) -> int:
+        return (step * self.world + self.rank) * self.seg_len
+
+    def first_output(self, step: int) -> int:
+        """Global index (in the halo-zero-padded stream's audio) of this rank's first output."""
+        return self.segment_start(step) // (self.decimation * self.audio_decimation)
+
+    @property
+    def next_rank(self) -> int:
+        return (self.rank + 1) % self.world
+
+    @property
+    def prev_rank(self) -> int:
+        return (self.rank - 1) % self.world
+
+
 class HaloRing:
     """Per-rank halo state and the per-step protocol.
 
-    halo:      the (T-1)-sample region directly in front of the segment (read by the head)
-    tail:      the segment's last T-1 samples (sent to the next rank)
+    halo:      the halo region directly in front of the segment (read by the head)
+    tail:      the segment's last halo-length samples (sent to the next rank)
     incoming:  rank 0 only (G > 1): receive buffer for the next step's halo
+    stage:     move the halo through host memory (a backend such as gloo that cannot send device
+               tensors, e.g. several ranks sharing one GPU in tests); RCCL sends device tensors
+               directly
     """
 
-    def __init__(self, geom: ShardGeometry, halo, tail, incoming=None):
+    def __init__(self, geom, halo, tail, incoming=None, stage: bool = False):
         self.geom, self.halo, self.tail, self.incoming = geom, halo, tail, incoming
         if geom.world > 1 and geom.rank == 0 and incoming is None:
             raise ValueError("rank 0 needs a receive buffer for the next step's halo")
+        self.stage = stage and getattr(tail, "is_cuda", False)
+        if self.stage:
+            import torch
+            self._send = torch.empty(tail.shape, dtype=tail.dtype, pin_memory=True)
+            self._recv = torch.empty(tail.shape, dtype=tail.dtype, pin_memory=True)
+
+    def _exchange(self, dst):
+        import torch.distributed as dist
+        g = self.geom
+        send, recv = self.tail, dst
+        if self.stage:
+            self._send.copy_(self.tail)  # synchronous: the tail is final once this returns
+            send, recv = self._send, self._recv
+        return dist.batch_isend_irecv([dist.P2POp(dist.isend, send, g.next_rank),
+                                       dist.P2POp(dist.irecv, recv, g.prev_rank)])
+
+    def _finish(self, reqs, dst):
+        for r in reqs:
+            r.wait()
+        if self.stage:
+            dst.copy_(self._recv)
 
     def step(self, bulk, head):
         """One sharded step. `bulk()` / `head()` launch the FIR over the segment-only outputs
@@ -96,17 +191,52 @@ class HaloRing:
             head()
             self.halo.copy_(self.tail)  # history carry for the next step
             return
-        import torch.distributed as dist
         dst = self.incoming if g.rank == 0 else self.halo
-        reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, self.tail, g.next_rank),
-                                       dist.P2POp(dist.irecv, dst, g.prev_rank)])
+        reqs = self._exchange(dst)
         bulk()
         if g.rank == 0:
             head()  # halo arrived during the previous step
-            for r in reqs:
-                r.wait()
+            self._finish(reqs, dst)
             self.halo.copy_(self.incoming)
         else:
-            for r in reqs:
-                r.wait()
+            self._finish(reqs, dst)
             head()
+
+
+class AmChainShard:
+    """One rank's state for the time-sharded AM receive chain (ChainShardGeometry) on the GPU:
+    buffer [halo | segment] of int8 IQ, the RF FIR + AM (gsdrInt8FirFCAmDemod) split into the bulk
+    (segment-only windows, launched while the halo exchange is in flight) and the head (windows
+    reaching into the halo), then the audio FIR (gsdrFirFF) over the step's AM samples.
+    Weak scaling: every rank processes seg_len samples per step."""
+
+    def __init__(self, geom: ChainShardGeometry, rf_taps, audio_taps, device, stage: bool = False):
+        import torch
+        self.geom, self.rf_taps, self.audio_taps = geom, rf_taps, audio_taps
+        H, L = geom.halo, geom.seg_len
+        self.buf = torch.zeros(2 * (H + L), dtype=torch.int8, device=device)
+        self.seg = self.buf[2 * H:]
+        incoming = (torch.zeros(2 * H, dtype=torch.int8, device=device)
+                    if geom.world > 1 and geom.rank == 0 else None)
+        self.ring = HaloRing(geom, self.buf[: 2 * H], self.seg[2 * (L - H):], incoming, stage)
+        self.am = torch.empty(geom.rf_outputs, dtype=torch.float32, device=device)
+        self.out = torch.empty(geom.outputs, dtype=torch.float32, device=device)
+
+    def _bulk(self):
+        from . import ops
+        g = self.geom
+        ops.fir(self.rf_taps, self.seg, g.decimation, g.rf_outputs - g.head_rf, out=self.am[g.head_rf:],
+                am=True, int8_iq=True)
+
+    def _head(self):
+        from . import ops
+        g = self.geom
+        ops.fir(self.rf_taps, self.buf, g.decimation, g.head_rf, out=self.am[: g.head_rf], am=True, int8_iq=True)
+
+    def step(self):
+        """One step over the segment currently in self.seg; the audio lands in self.out."""
+        from . import ops
+        g = self.geom
+        self.ring.step(self._bulk, self._head)
+        ops.fir(self.audio_taps, self.am, g.audio_decimation, g.outputs, out=self.out)
+        return self.out

@@ -1,0 +1,118 @@
+"""Time-sharded streams on the HIP kernels: two ranks (gloo, halos staged through host memory),
+both on cuda:0, run the ring-halo protocol of gpusdr/shard.py with the real gfx950 FIR kernels -
+C4's shape (cf32, 1023 taps, D = 1, bulk / head launches) and the C5 AM receive chain with its
+cascaded halo ((Ta - 1) D + T - 1 samples, AmChainShard). The concatenated per-rank outputs must
+equal the float64 oracle over the whole stream within the FIR tolerance 1e-6 * sum|h||x|
+(SURVEY.md 8d), i.e. sharding changes nothing but where work runs. The stream is primed: rank 0's
+first halo holds the stream's first samples (as a live receiver's history would), so no window
+is artificially zero-padded.
+The same code runs over RCCL with one GPU per rank in bench.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIR_TOL = 1e-6
+WORLD, STEPS = 2, 3
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, kind, out_dir):
+    import sys
+    sys.path[:0] = [os.path.join(REPO, "cuda-sdr_amd"), os.path.join(REPO, "oracle")]
+    import torch
+    import torch.distributed as dist
+
+    import oracle as orc
+    from gpusdr import ops
+    from gpusdr.shard import AmChainShard, ChainShardGeometry, HaloRing, ShardGeometry
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    outs = []
+    if kind == "c4":
+        T, D, L = 1023, 1, 20_000
+        geom = ShardGeometry(rank, world, L, T, D)
+        taps = torch.from_numpy(orc.lowpass_taps(T, 0.04, "blackman")).to(dev)
+        H = geom.halo
+        buf = torch.zeros(H + L, dtype=torch.complex64, device=dev)
+        seg = buf[H:]
+        incoming = torch.zeros(H, dtype=torch.complex64, device=dev) if rank == 0 else None
+        ring = HaloRing(geom, buf[:H], seg[L - H:], incoming, stage=True)
+        y = torch.empty(geom.outputs, dtype=torch.complex64, device=dev)
+        hb = geom.head_outputs
+        if rank == 0:
+            ops.synth_wideband_cf32(0xC4, 0.013, 0.31, 0, H, out=buf[:H])  # primed history
+        for step in range(STEPS):
+            ops.synth_wideband_cf32(0xC4, 0.013, 0.31, H + geom.segment_start(step), L, out=seg)
+            ring.step(lambda: ops.fir(taps, seg[geom.bulk_input_offset():], D, geom.outputs - hb, out=y[hb:]),
+                      lambda: ops.fir(taps, buf, D, hb, out=y[:hb]))
+            torch.cuda.synchronize()
+            outs.append(y.cpu().numpy().copy())
+    else:
+        T, D, Ta, Da, L = 1023, 10, 255, 20, 40_000
+        geom = ChainShardGeometry(rank, world, L, T, D, Ta, Da)
+        rf = torch.from_numpy(orc.lowpass_taps(T, 0.04, "blackman")).to(dev)
+        au = torch.from_numpy(orc.lowpass_taps(Ta, 0.02)).to(dev)
+        sh = AmChainShard(geom, rf, au, dev, stage=True)
+        H = geom.halo
+        if rank == 0:
+            ops.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, H, out=sh.buf[: 2 * H])  # primed history
+        for step in range(STEPS):
+            ops.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, H + geom.segment_start(step), L, out=sh.seg)
+            out = sh.step()
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy().copy())
+    np.save(os.path.join(out_dir, f"{kind}_rank{rank}.npy"), np.stack(outs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(kind, tmp_path):
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_main, args=(WORLD, _free_port(), kind, str(tmp_path)), nprocs=WORLD, join=True,
+                       start_method="spawn")
+    per = [np.load(os.path.join(tmp_path, f"{kind}_rank{r}.npy")) for r in range(WORLD)]
+    return np.concatenate([per[r][s] for s in range(STEPS) for r in range(WORLD)])
+
+
+def test_c4_shape_time_sharded_on_hip(tmp_path, orc):
+    T, D, L = 1023, 1, 20_000
+    got = _run("c4", tmp_path)
+    n = L * WORLD * STEPS
+    stream = orc.synth_wideband_cf32(0xC4, 0.013, 0.31, 0, T - 1 + n)
+    y64, bound = orc.fir_f64(orc.lowpass_taps(T, 0.04, "blackman"), stream, D, n // D)
+    assert len(got) == len(y64)
+    err = np.abs(got.astype(np.complex128) - y64)
+    assert np.all(err <= FIR_TOL * bound + 1e-30), float(np.max(err / (bound + 1e-30)))
+
+
+def test_c5_chain_time_sharded_cascaded_halo(tmp_path, orc):
+    from gpusdr.shard import ChainShardGeometry
+    T, D, Ta, Da, L = 1023, 10, 255, 20, 40_000
+    H = ChainShardGeometry(0, WORLD, L, T, D, Ta, Da).halo
+    assert H == 3600  # (Ta - 1) D + T - 1 = 3562, rounded up to a multiple of D Da
+    got = _run("c5", tmp_path)
+    padded = orc.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, H + L * WORLD * STEPS)  # primed stream
+    rf, au = orc.lowpass_taps(T, 0.04, "blackman"), orc.lowpass_taps(Ta, 0.02)
+    x = orc.int8_to_float(padded).view(np.complex64)
+    y, rf_bound = orc.fir_f64(rf, x, D)
+    am = np.abs(y)
+    want, audio_bound = orc.fir_f64(au, am.astype(np.float32), Da)
+    n = len(got)
+    assert n == L * WORLD * STEPS // (D * Da) and len(want) >= n
+    carried, _ = orc.fir_f64(np.abs(au), (FIR_TOL * (rf_bound + am)).astype(np.float32), Da, n)
+    bound = carried + FIR_TOL * audio_bound[:n] + 1e-30
+    assert np.all(np.abs(got - want[:n]) <= bound)
