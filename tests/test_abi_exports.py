@@ -53,3 +53,33 @@ def test_library_loads_without_gpu(built):
             "assert L.gsdrFirFC and L.gsdrInt8FirFCAmDemod; print('ok')")
     r = subprocess.run([sys.executable, "-c", code, built], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
+
+
+# Every public header path of the reference's include/gpusdrpipeline that a drop-in caller may
+# include (the reference's application-only headers SdrSession.h, am.h, fm.h and
+# util/{ScopeExit,Thread,Window}.h are outside the hot path and not provided).
+REFERENCE_HEADER_PATHS = [
+    "CudaErrors.h", "Factories.h", "GSDefs.h", "GSErrors.h", "GSLog.h", "IMemory.h", "IRef.h",
+    "Modulation.h", "Result.h", "SampleType.h", "Status.h", "util/CudaDevicePushPop.h", "util/CudaUtil.h",
+]
+
+
+def test_reference_header_paths_compile(tmp_path):
+    """The reference's include paths exist and compile; the CUDA-named error / device-scope
+    macros of CudaErrors.h and util/CudaDevicePushPop.h forward to the HIP ones."""
+    src = tmp_path / "inc.cpp"
+    body = "".join(f"#include <gpusdrpipeline/{h}>\n" for h in REFERENCE_HEADER_PATHS)
+    body += """#include <stdexcept>
+Status f(int d) {
+  CUDA_DEV_PUSH_POP_OR_RET_STATUS(d);
+  SAFE_CUDA_OR_RET_STATUS(hipDeviceSynchronize());
+  CHECK_CUDA_OR_RET_STATUS("launch");
+  return cudaErrorToStatus(hipErrorInvalidValue);
+}
+int main() { CudaDevicePushPop p(0); (void)p; return 0; }
+"""
+    src.write_text(body)
+    r = subprocess.run(["/opt/rocm/lib/llvm/bin/clang++", "-std=c++20", "-fsyntax-only", "-D__HIP_PLATFORM_AMD__",
+                        "-I/opt/rocm/include", "-I" + os.path.join(REPO, "include"), str(src)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
