@@ -4,7 +4,10 @@
 #include <gpusdrpipeline/Factories.h>
 #include <gpusdrpipeline/abi/errors.h>
 
+#include <algorithm>
 #include <vector>
+
+#include "../runtime/composite.h"
 
 namespace {
 
@@ -36,7 +39,7 @@ uint32_t give(RefResult<T>&& r, gspHandle* out) {
   return Status_Success;
 }
 
-uint32_t push(gspHandle node, size_t port, const void* src, size_t bytes, gspHandle queue, hipMemcpyKind kind) {
+uint32_t push(gspHandle node, size_t port, const void* src, size_t bytes, gspHandle queue) {
   Sink* sink = as<Sink>(node);
   ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
   if (sink == nullptr || q == nullptr || (src == nullptr && bytes != 0)) return Status_InvalidArgument;
@@ -44,7 +47,9 @@ uint32_t push(gspHandle node, size_t port, const void* src, size_t bytes, gspHan
   UNWRAP_OR_FWD_STATUS(b, sink->requestBuffer(port, bytes));
   if (bytes != 0) {
     HIP_DEV_PUSH_POP_OR_RET_STATUS(q->cudaDevice());
-    const hipError_t e = hipMemcpyAsync(b.get()->writePtr(), src, bytes, kind, q->cudaStream());
+    // the lent window is device memory, or pinned host memory (the H2D staging filter): the copy
+    // direction comes from the pointers (unified addressing)
+    const hipError_t e = hipMemcpyAsync(b.get()->writePtr(), src, bytes, hipMemcpyDefault, q->cudaStream());
     if (e != hipSuccess) {
       (void)sink->commitBuffer(port, 0);  // cancel the checkout
       return hipErrorToStatus(e);
@@ -122,11 +127,11 @@ uint32_t gspNodeCreate(const char* name, const char* json, gspHandle* nodeOut) {
 }
 
 uint32_t gspSinkPushHost(gspHandle node, size_t port, const void* host, size_t bytes, gspHandle queue) {
-  return push(node, port, host, bytes, queue, hipMemcpyHostToDevice);
+  return push(node, port, host, bytes, queue);
 }
 
 uint32_t gspSinkPushDevice(gspHandle node, size_t port, const void* device, size_t bytes, gspHandle queue) {
-  return push(node, port, device, bytes, queue, hipMemcpyDeviceToDevice);
+  return push(node, port, device, bytes, queue);
 }
 
 uint32_t gspSinkPreferredInputSize(gspHandle node, size_t port, size_t* bytesOut) {
@@ -168,6 +173,30 @@ uint32_t gspBufferCreate(gspHandle queue, size_t bytes, gspHandle* bufferOut) {
   return give(bf.get()->createBuffer(bytes), bufferOut);
 }
 
+uint32_t gspHostBufferCreate(gspHandle queue, size_t bytes, gspHandle* bufferOut) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (q == nullptr) return Status_InvalidArgument;
+  Ref<IAllocator> alloc;
+  Ref<IBufferFactory> bf;
+  UNWRAP_OR_FWD_STATUS(alloc, factories()->getCudaAllocatorFactory()->createCudaAllocator(q, 32, true));
+  UNWRAP_OR_FWD_STATUS(bf, factories()->createBufferFactory(alloc.get().get()));
+  return give(bf.get()->createBuffer(bytes), bufferOut);
+}
+
+uint32_t gspDesignLowPass(double sampleRate, double cutoff, double transitionWidth, double dbAttenuation, float* taps,
+                          size_t capacity, size_t* countOut) {
+  std::vector<float> t;
+  try {
+    FWD_IF_ERR(gsdr_rt::designLowPass(sampleRate, cutoff, transitionWidth, dbAttenuation, t));
+  } catch (...) {
+    return Status_OutOfMemory;
+  }
+  if (countOut) *countOut = t.size();
+  if (taps == nullptr || capacity < t.size()) return taps == nullptr ? Status_Success : Status_OutOfRange;
+  std::copy(t.begin(), t.end(), taps);
+  return Status_Success;
+}
+
 uint32_t gspBufferSlice(gspHandle buffer, size_t start, size_t end, gspHandle* sliceOut) {
   IBuffer* b = as<IBuffer>(buffer);
   if (b == nullptr) return Status_InvalidArgument;
@@ -200,7 +229,7 @@ uint32_t gspBufferToHost(gspHandle buffer, void* host, size_t bytes, gspHandle q
   if (b == nullptr || q == nullptr || (host == nullptr && bytes != 0)) return Status_InvalidArgument;
   const size_t n = bytes < b->range()->used() ? bytes : b->range()->used();
   HIP_DEV_PUSH_POP_OR_RET_STATUS(q->cudaDevice());
-  if (n != 0) SAFE_HIP_OR_RET_STATUS(hipMemcpyAsync(host, b->readPtr(), n, hipMemcpyDeviceToHost, q->cudaStream()));
+  if (n != 0) SAFE_HIP_OR_RET_STATUS(hipMemcpyAsync(host, b->readPtr(), n, hipMemcpyDefault, q->cudaStream()));
   SAFE_HIP_OR_RET_STATUS(hipStreamSynchronize(q->cudaStream()));
   return Status_Success;
 }

@@ -52,6 +52,8 @@ def _L():
             "gspSourceOutputSize": ([h, sz, psz, psz], u32),
             "gspSourceRead": ([h, ph, sz], u32),
             "gspBufferCreate": ([h, sz, ph], u32),
+            "gspHostBufferCreate": ([h, sz, ph], u32),
+            "gspDesignLowPass": ([ctypes.c_double] * 4 + [vp, sz, psz], u32),
             "gspBufferSlice": ([h, sz, sz, ph], u32),
             "gspBufferRange": ([h, psz, psz, psz], u32),
             "gspBufferSetRange": ([h, sz, sz], u32),
@@ -136,6 +138,11 @@ class Buffer(_Handle):
     def create(cls, queue: Queue, nbytes: int) -> "Buffer":
         return cls(_create(_L().gspBufferCreate, queue.handle, nbytes, what="gspBufferCreate"), queue)
 
+    @classmethod
+    def create_host(cls, queue: Queue, nbytes: int) -> "Buffer":
+        """Pinned host memory (the output side of a device -> host staging filter)."""
+        return cls(_create(_L().gspHostBufferCreate, queue.handle, nbytes, what="gspHostBufferCreate"), queue)
+
     def slice(self, start: int, end: int) -> "Buffer":
         return Buffer(_create(_L().gspBufferSlice, self._h, start, end, what="gspBufferSlice"), self.queue, self)
 
@@ -159,6 +166,18 @@ class Buffer(_Handle):
         out = np.empty(n, dtype=np.uint8)
         _check(_L().gspBufferToHost(self._h, out.ctypes.data, n, self.queue.handle), "gspBufferToHost")
         return out.view(dtype)
+
+
+def design_lowpass(sample_rate: float, cutoff: float, transition: float, db_attenuation: float) -> np.ndarray:
+    """The RF -> PCM component's low-pass designer (gspDesignLowPass; Kaiser window at the
+    reference's fred harris length)."""
+    n = ctypes.c_size_t()
+    _check(_L().gspDesignLowPass(sample_rate, cutoff, transition, db_attenuation, None, 0, ctypes.byref(n)),
+           "gspDesignLowPass")
+    taps = np.empty(n.value, dtype=np.float32)
+    _check(_L().gspDesignLowPass(sample_rate, cutoff, transition, db_attenuation, taps.ctypes.data, len(taps),
+                                 ctypes.byref(n)), "gspDesignLowPass")
+    return taps
 
 
 class Node(_Handle):

@@ -67,12 +67,21 @@ GSP_API uint32_t gspSourceRead(gspHandle node, gspHandle* buffers, size_t buffer
 
 /* Device buffers (32-byte aligned device memory from the queue's stream-ordered pool). */
 GSP_API uint32_t gspBufferCreate(gspHandle queue, size_t bytes, gspHandle* bufferOut);
+/* Pinned host buffers (hipHostMalloc through the queue's allocator): outputs of the D2H staging
+ * filter. gspBufferBase is then a host pointer. */
+GSP_API uint32_t gspHostBufferCreate(gspHandle queue, size_t bytes, gspHandle* bufferOut);
 GSP_API uint32_t gspBufferSlice(gspHandle buffer, size_t start, size_t end, gspHandle* sliceOut);
 GSP_API uint32_t gspBufferRange(gspHandle buffer, size_t* offset, size_t* endOffset, size_t* capacity);
 GSP_API uint32_t gspBufferSetRange(gspHandle buffer, size_t offset, size_t endOffset);
 GSP_API void* gspBufferBase(gspHandle buffer);
 /* Copies the buffer's used bytes (at most `bytes`) to host and synchronises the queue. */
 GSP_API uint32_t gspBufferToHost(gspHandle buffer, void* host, size_t bytes, gspHandle queue);
+
+/* The RF -> PCM component's low-pass designer (Kaiser window, runtime/composite.h; the reference's
+ * remez is not vendored): writes the taps if `taps` holds `capacity` >= count floats; *countOut =
+ * the tap count. taps == nullptr only reports the count. */
+GSP_API uint32_t gspDesignLowPass(double sampleRate, double cutoff, double transitionWidth, double dbAttenuation,
+                                  float* taps, size_t capacity, size_t* countOut);
 
 /* SteppingDriver (ISteppingDriver, SteppingDriver.cpp:102-366): connect nodes, name them, and
  * pull one step of every graph tail. Handles are nodes from the creators above. */
