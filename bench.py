@@ -306,12 +306,8 @@ class AmChainRunner:
                 ev[0].record(self.stream)
             if self.mode == "resident":
                 self.chain.step_resident(self.iq, self.chunks, self.out)
-            else:
-                n = C5_CHUNK // (self.D * self.Da)
-                pos = 0
-                for c in range(self.chunks):
-                    got = self.chain.step(self.iq[2 * C5_CHUNK * c: 2 * C5_CHUNK * (c + 1)], self.out[pos: pos + n])
-                    pos += got.numel()
+            else:  # live-stream chunks, all of a step's chunk steps as one cached graph launch
+                self.chain.step_chunks(self.iq, self.chunks, self.out)
             if ev is not None:
                 ev[1].record(self.stream)
 

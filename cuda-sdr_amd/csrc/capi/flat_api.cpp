@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../runtime/composite.h"
+#include "../runtime/driver.h"
 
 namespace {
 
@@ -252,6 +253,23 @@ uint32_t gspDriverSetupNode(gspHandle driver, gspHandle node, const char* name) 
   Node* n = as<Node>(node);
   if (d == nullptr || n == nullptr) return Status_InvalidArgument;
   return d->setupNode(n, name);
+}
+
+uint32_t gspDriverDoFilterGraphed(gspHandle driver, gspHandle queue) {
+  auto* d = dynamic_cast<gsdr_rt::SteppingDriver*>(as<IDriver>(driver));
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (d == nullptr || q == nullptr) return Status_InvalidArgument;
+  return d->doFilterGraphed(q->cudaStream());
+}
+
+uint32_t gspDriverGraphStats(gspHandle driver, size_t* eager, size_t* captured, size_t* replayed) {
+  auto* d = dynamic_cast<gsdr_rt::SteppingDriver*>(as<IDriver>(driver));
+  if (d == nullptr) return Status_InvalidArgument;
+  const auto st = d->graphStats();
+  if (eager) *eager = st.eager;
+  if (captured) *captured = st.captured;
+  if (replayed) *replayed = st.replayed;
+  return Status_Success;
 }
 
 uint32_t gspDriverDoFilter(gspHandle driver) {

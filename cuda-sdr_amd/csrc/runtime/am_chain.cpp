@@ -69,6 +69,12 @@ struct gsdrAmChainImpl {
   float* resOut = nullptr;
   size_t resChunks = 0;
   bool resFirst = false;
+  // multi-chunk stepping (gsdrAmChainStepChunks): one cached graph of nChunks chunk steps
+  hipGraphExec_t multi = nullptr;
+  const int8_t* multiIn = nullptr;
+  float* multiOut = nullptr;
+  size_t multiChunks = 0;
+  int multiKey = -1;  // 2 = starts with the first step, else the starting parity
   // pinned ring
   size_t slots = 0;
   int8_t* hostIn = nullptr;
@@ -119,6 +125,21 @@ struct gsdrAmChainImpl {
     return hipSuccess;
   }
 
+  // nChunks consecutive chunk steps from `in` (device, contiguous chunks), audio appended at `out`
+  hipError_t enqueueChunks(const int8_t* in, size_t nChunks, float* out, size_t startStep) {
+    size_t pos = 0;
+    for (size_t i = 0; i < nChunks; ++i) {
+      const size_t step = startStep + i;
+      const int p = step == 0 ? 0 : (int)(step & 1);
+      const size_t n = step == 0 ? na1 : naSteady;
+      AMC_TRY(hipMemcpyAsync(staging[p] + 2 * r, in + 2 * L * i, 2 * L, hipMemcpyDeviceToDevice, stream));
+      AMC_TRY(enqueueCompute(step == 0, p));
+      AMC_TRY(hipMemcpyAsync(out + pos, audio, sizeof(float) * n, hipMemcpyDeviceToDevice, stream));
+      pos += n;
+    }
+    return hipSuccess;
+  }
+
   void release() {
     if (stream != nullptr) (void)hipStreamSynchronize(stream);
     if (copyStream != nullptr) (void)hipStreamSynchronize(copyStream);
@@ -138,6 +159,7 @@ struct gsdrAmChainImpl {
     (void)hipFree(am);
     (void)hipFree(amBig);
     if (resident) (void)hipGraphExecDestroy(resident);
+    if (multi) (void)hipGraphExecDestroy(multi);
     (void)hipFree(audio);
     if (hostIn) (void)hipHostFree(hostIn);
     if (hostOut) (void)hipHostFree(hostOut);
@@ -253,6 +275,47 @@ hipError_t gsdrAmChainStep(gsdrAmChain c, const int8_t* inputIq, float* output, 
   AMC_TRY(hipEventRecord(c->readDone[p], c->stream));
   AMC_TRY(hipMemcpyAsync(output, c->audio, sizeof(float) * n, hipMemcpyDeviceToDevice, c->stream));
   ++c->steps;
+  if (outputCount != nullptr) *outputCount = n;
+  return hipSuccess;
+}
+
+size_t gsdrAmChainChunksOutputCount(gsdrAmChain c, size_t nChunks) {
+  if (c == nullptr || nChunks == 0) return 0;
+  return c->steps == 0 ? c->na1 + (nChunks - 1) * c->naSteady : nChunks * c->naSteady;
+}
+
+hipError_t gsdrAmChainStepChunks(gsdrAmChain c, const int8_t* inputIq, size_t nChunks, float* output,
+                                 size_t* outputCount) {
+  if (c == nullptr || inputIq == nullptr || output == nullptr || nChunks == 0) return hipErrorInvalidValue;
+  DevicePush push(c->device);
+  AMC_TRY(push.err);
+  const size_t n = gsdrAmChainChunksOutputCount(c, nChunks);
+  const int key = c->steps == 0 ? 2 : (int)(c->steps & 1);
+  if (c->multi == nullptr || c->multiIn != inputIq || c->multiOut != output || c->multiChunks != nChunks ||
+      c->multiKey != key) {
+    if (c->multi != nullptr) {
+      AMC_TRY(hipStreamSynchronize(c->stream));
+      AMC_TRY(hipGraphExecDestroy(c->multi));
+      c->multi = nullptr;
+    }
+    hipGraph_t g = nullptr;
+    AMC_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    hipError_t e = c->enqueueChunks(inputIq, nChunks, output, c->steps);
+    const hipError_t e2 = hipStreamEndCapture(c->stream, &g);
+    if (e == hipSuccess) e = e2;
+    if (e == hipSuccess) e = hipGraphInstantiate(&c->multi, g, nullptr, nullptr, 0);
+    if (g != nullptr) (void)hipGraphDestroy(g);
+    AMC_TRY(e);
+    c->multiIn = inputIq;
+    c->multiOut = output;
+    c->multiChunks = nChunks;
+    c->multiKey = key;
+  }
+  AMC_TRY(hipGraphLaunch(c->multi, c->stream));
+  // both staging parities were last read by this launch
+  AMC_TRY(hipEventRecord(c->readDone[0], c->stream));
+  AMC_TRY(hipEventRecord(c->readDone[1], c->stream));
+  c->steps += nChunks;
   if (outputCount != nullptr) *outputCount = n;
   return hipSuccess;
 }

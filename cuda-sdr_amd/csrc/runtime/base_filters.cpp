@@ -3,6 +3,8 @@
 #include <gpusdrpipeline/abi/base_filters.h>
 #include <gpusdrpipeline/abi/errors.h>
 
+#include "buffers.h"
+
 namespace {
 constexpr size_t kInitialPortBytes = 8192;  // BaseSink.cpp:47-59
 }
@@ -97,6 +99,21 @@ Status BaseSink::consumeInputBytesAndMoveUsedToStart(size_t port, size_t numByte
   FWD_IF_ERR(b->range()->increaseOffset(numBytes));
   if (b->range()->used() == 0) (void)b->range()->setUsedRange(0, 0);  // empty window: rewind for free
   return Status_Success;
+}
+
+void BaseSink::foldWindowState(uint64_t& h) const noexcept {
+  auto mix = [&h](uint64_t v) { h = (h ^ v) * 0x100000001B3ull + 0x9E3779B97F4A7C15ull; };
+  mix(mInputPorts.size());
+  for (const InputPort& p : mInputPorts) {
+    const IRelocatableResizableBuffer* b = p.inputBuffer.get();
+    mix(reinterpret_cast<uintptr_t>(b->base()));
+    const auto* rb = dynamic_cast<const gsdr_rt::RelocatableResizableBuffer*>(b);
+    mix(rb != nullptr ? reinterpret_cast<uintptr_t>(rb->spareBase()) : 1);
+    mix(b->range()->offset());
+    mix(b->range()->endOffset());
+    mix(b->range()->capacity());
+    mix(p.bufferCheckedOut ? 1 : 0);
+  }
 }
 
 BaseSource::BaseSource(std::vector<ImmutableRef<IBufferCopier>>&& outputPortBufferCopiers) noexcept

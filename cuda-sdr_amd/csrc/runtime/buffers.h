@@ -180,6 +180,9 @@ class BufferSliceFactory final : public IBufferSliceFactory {
 // Growable window with a spare allocation so relocate() never copies onto itself.
 class RelocatableResizableBuffer final : public IRelocatableResizableBuffer {
  public:
+  // the spare allocation relocate() copies into (graph stepping folds it into a window's state:
+  // the first relocation allocates it)
+  const void* spareBase() const noexcept { return mSpare != nullptr ? mSpare.get()->data() : nullptr; }
   static Result<IRelocatableResizableBuffer> create(size_t size, IAllocator* allocator, const IBufferCopier* copier,
                                                     const IBufferRangeFactory* ranges) noexcept;
   uint8_t* base() noexcept final { return mData == nullptr ? nullptr : mData->data(); }

@@ -3,8 +3,10 @@
 #include "driver.h"
 
 #include "buffers.h"
+#include "graph_state.h"
 
 #include <gpusdrpipeline/abi/errors.h>
+#include <gsdr/gsdr_amd.h>
 
 #include <algorithm>
 #include <cstring>
@@ -291,6 +293,100 @@ Status SteppingDriver::doSourceOutput(Source* source) {
   }
   mBufferRefs.clear();
   return Status_Success;
+}
+
+// ---- graph stepping -----------------------------------------------------------------------------
+// The steady state of a chain fed fixed-size chunks repeats: every node's window sits at one of a
+// few placements (lazy compaction cycles through them), and a step from a given placement enqueues
+// the same launches with the same arguments. So the step's device work is captured once per
+// placement and replayed. The host bookkeeping (window offsets, consume, commit) must still
+// advance, so a replayed step runs doFilter() under a stream capture that is thrown away - the
+// host logic runs, its launches are recorded instead of executed - and then launches the cached
+// executable graph: one launch instead of one per kernel / copy. A placement is captured only
+// the second time it is seen (the first time may still grow windows: allocation, no replay), and
+// the driver falls back to plain steps for good when a chain's state does not repeat (a tone
+// source's phase) or a node is not on `stream`.
+
+SteppingDriver::~SteppingDriver() {
+  for (const CachedGraph& g : mGraphs) (void)hipGraphExecDestroy(g.exec);
+}
+
+bool SteppingDriver::chainState(hipStream_t stream, uint64_t& key) const noexcept {
+  uint64_t h = 0xCBF29CE484222325ull ^ (uint64_t)gsdrAmdGetKernelPolicy();
+  // every connected node (a fixed order: by address)
+  std::vector<Node*> nodes;
+  for (Source* so : mSourceOrder) nodes.push_back(so);
+  for (const auto& kv : mSinks) nodes.push_back(kv.first);
+  std::sort(nodes.begin(), nodes.end());
+  nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
+  if (nodes.empty()) return false;
+  for (Node* n : nodes) {
+    const auto* g = dynamic_cast<const IGraphStepState*>(n);
+    if (g == nullptr || g->graphStream() != stream || !g->graphState(h)) return false;
+    h = (h ^ reinterpret_cast<uintptr_t>(n)) * 0x100000001B3ull;
+  }
+  key = h;
+  return true;
+}
+
+Status SteppingDriver::captureStep(hipStream_t stream, hipGraph_t* graphOut) noexcept {
+  *graphOut = nullptr;
+  SAFE_HIP_OR_RET_STATUS(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+  const Status st = doFilter();
+  const hipError_t e = hipStreamEndCapture(stream, graphOut);
+  if (st != Status_Success) {
+    if (*graphOut != nullptr) (void)hipGraphDestroy(*graphOut);
+    *graphOut = nullptr;
+    return st;
+  }
+  SAFE_HIP_OR_RET_STATUS(e);
+  return Status_Success;
+}
+
+Status SteppingDriver::doFilterGraphed(hipStream_t stream) noexcept {
+  try {
+    uint64_t key = 0;
+    if (mGraphOff || stream == nullptr || !chainState(stream, key)) {
+      ++mStats.eager;
+      return doFilter();
+    }
+    for (const CachedGraph& g : mGraphs) {
+      if (g.key != key) continue;
+      hipGraph_t scratch = nullptr;  // host bookkeeping only; the recorded launches are discarded
+      FWD_IF_ERR(captureStep(stream, &scratch));
+      if (scratch != nullptr) (void)hipGraphDestroy(scratch);
+      SAFE_HIP_OR_RET_STATUS(hipGraphLaunch(g.exec, stream));
+      ++mStats.replayed;
+      mGraphMisses = 0;
+      return Status_Success;
+    }
+    if (std::find(mSeen.begin(), mSeen.end(), key) == mSeen.end()) {
+      if (mSeen.size() >= 64 || ++mGraphMisses > 32) {
+        mGraphOff = true;  // the state does not repeat: plain steps from now on
+      } else {
+        mSeen.push_back(key);
+      }
+      ++mStats.eager;
+      return doFilter();
+    }
+    if (mGraphs.size() >= 16) {  // more placements than a steady state cycles through
+      mGraphOff = true;
+      ++mStats.eager;
+      return doFilter();
+    }
+    hipGraph_t graph = nullptr;
+    FWD_IF_ERR(captureStep(stream, &graph));
+    if (graph == nullptr) return Status_RuntimeError;
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    SAFE_HIP_OR_RET_STATUS(ie);
+    mGraphs.push_back(CachedGraph{key, exec});
+    SAFE_HIP_OR_RET_STATUS(hipGraphLaunch(exec, stream));
+    ++mStats.captured;
+    return Status_Success;
+  }
+  IF_CATCH_RETURN_STATUS;
 }
 
 }  // namespace gsdr_rt

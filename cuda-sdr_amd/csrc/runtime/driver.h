@@ -9,9 +9,14 @@
 //  * node names are looked up only when a message is logged (the reference builds std::string
 //    names on every step, :208-217);
 //  * a cycle in the graph ends the step with Status_InvalidState instead of recursing forever.
+//
+// MI355X extension: doFilterGraphed(stream) - the same step, with its device work replayed from a
+// captured hipGraph once the chain's host state repeats (see driver.cpp).
 #pragma once
 
 #include <gpusdrpipeline/Factories.h>
+
+#include <hip/hip_runtime_api.h>
 
 #include <string>
 #include <unordered_map>
@@ -37,6 +42,17 @@ class SteppingDriver final : public ISteppingDriver {
                                                           const char* attrVal) noexcept) noexcept final;
   size_t getNodeName(Node* node, char* name, size_t nameBufLen, bool* foundOut) noexcept final;
   Status doFilter() noexcept final;
+
+  // One doFilter() step; when every node is a graph-steppable filter on `stream` and the chain's
+  // host state (window placement of every node) has been seen before, the step's device work is
+  // captured once into a hipGraph keyed by that state and replayed from then on.
+  Status doFilterGraphed(hipStream_t stream) noexcept;
+  struct GraphStats {
+    size_t eager = 0;     // steps run as plain launches
+    size_t captured = 0;  // steps that captured (and launched) a new graph
+    size_t replayed = 0;  // steps whose device work was a cached graph launch
+  };
+  GraphStats graphStats() const noexcept { return mStats; }
 
  private:
   struct SinkPortKey {
@@ -81,8 +97,21 @@ class SteppingDriver final : public ISteppingDriver {
   std::vector<Ref<IBuffer>> mBufferRefs;
   std::vector<IBuffer*> mPortBuffers;
   std::vector<Ref<IBuffer>> mViewRefs;  // capped fan-out views (doSourceOutput)
+  // graph stepping
+  struct CachedGraph {
+    uint64_t key;
+    hipGraphExec_t exec;
+  };
+  std::vector<CachedGraph> mGraphs;
+  std::vector<uint64_t> mSeen;
+  size_t mGraphMisses = 0;
+  bool mGraphOff = false;
+  GraphStats mStats;
+  bool chainState(hipStream_t stream, uint64_t& key) const noexcept;
+  Status captureStep(hipStream_t stream, hipGraph_t* graphOut) noexcept;
 
-  REF_COUNTED(SteppingDriver);
+  ~SteppingDriver() final;
+  REF_COUNTED_NO_DESTRUCTOR(SteppingDriver);
 };
 
 class SteppingDriverFactory final : public ISteppingDriverFactory {

@@ -427,14 +427,14 @@ Result<Filter> HipMemcpyFilter::create(hipMemcpyKind kind, ICudaCommandQueue* qu
   std::vector<ImmutableRef<IBufferCopier>> copiers;
   UNWRAP_MOVE_OR_FWD_RESULT(copiers, deviceOutputCopiers(factories, queue));
   return makeRefResultNonNull<Filter>(new (std::nothrow) HipMemcpyFilter(
-      windows.get().get(), factories->getBufferSliceFactory(), memSet.get().get(), copier.get().get(),
+      windows.get().get(), factories->getBufferSliceFactory(), memSet.get().get(), copier.get().get(), queue,
       std::move(copiers)));
 }
 
 HipMemcpyFilter::HipMemcpyFilter(IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
-                                 IMemSet* memSet, IBufferCopier* copier,
+                                 IMemSet* memSet, IBufferCopier* copier, ICudaCommandQueue* queue,
                                  std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept
-    : BaseFilter(windows, slices, 1, std::move(outputCopiers), memSet), mCopier(copier) {}
+    : BaseFilter(windows, slices, 1, std::move(outputCopiers), memSet), mCopier(copier), mQueue(queue) {}
 
 size_t HipMemcpyFilter::getOutputDataSize(size_t port) noexcept {
   GS_REQUIRE_OR_RET_FMT(port == 0, 0, "Output port [%zu] is out of range", port);

@@ -9,14 +9,22 @@
 #include <gpusdrpipeline/abi/base_filters.h>
 #include <gpusdrpipeline/abi/errors.h>
 
+#include "graph_state.h"
+
 namespace gsdr_rt {
 
 // Bytes per element of each SampleType on a filter's *input* side. Int8Complex is one I/Q
 // pair (2 bytes); the reference's 1-byte size (Fir.cpp:34-45) never produced output.
 size_t inputElementSize(SampleType t) noexcept;
 
-class Fir final : public BaseFilter {
+class Fir final : public BaseFilter, public IGraphStepState {
  public:
+  hipStream_t graphStream() const noexcept final { return mQueue->cudaStream(); }
+  bool graphState(uint64_t& h) const noexcept final {
+    foldWindowState(h);
+    h = (h ^ reinterpret_cast<uintptr_t>(mTaps.get() ? mTaps->data() : nullptr)) * 0x100000001B3ull + mTapCount;
+    return true;
+  }
   static Result<Filter> create(SampleType tapType, SampleType elementType, size_t decimation, const float* taps,
                                size_t tapCount, ICudaCommandQueue* queue, IFactories* factories) noexcept;
 
@@ -50,8 +58,13 @@ class Fir final : public BaseFilter {
   REF_COUNTED(Fir);
 };
 
-class QuadAmDemod final : public BaseFilter {
+class QuadAmDemod final : public BaseFilter, public IGraphStepState {
  public:
+  hipStream_t graphStream() const noexcept final { return mQueue->cudaStream(); }
+  bool graphState(uint64_t& h) const noexcept final {
+    foldWindowState(h);
+    return true;
+  }
   static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
@@ -67,8 +80,13 @@ class QuadAmDemod final : public BaseFilter {
 
 // Two-input complex multiply (Multiply.cpp:26-159): the frequency shifter's mixer when port 1 is
 // fed by a ComplexCosine source.
-class MultiplyCcc final : public BaseFilter {
+class MultiplyCcc final : public BaseFilter, public IGraphStepState {
  public:
+  hipStream_t graphStream() const noexcept final { return mQueue->cudaStream(); }
+  bool graphState(uint64_t& h) const noexcept final {
+    foldWindowState(h);
+    return true;
+  }
   static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
@@ -85,8 +103,13 @@ class MultiplyCcc final : public BaseFilter {
 
 // Quadrature FM discriminator (QuadFmDemod.cpp:28-115): n inputs -> n - 1 outputs, the last input
 // kept for the next call.
-class QuadFmDemod final : public BaseFilter {
+class QuadFmDemod final : public BaseFilter, public IGraphStepState {
  public:
+  hipStream_t graphStream() const noexcept final { return mQueue->cudaStream(); }
+  bool graphState(uint64_t& h) const noexcept final {
+    foldWindowState(h);
+    return true;
+  }
   static Result<Filter> create(float gain, ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
@@ -102,8 +125,13 @@ class QuadFmDemod final : public BaseFilter {
   REF_COUNTED(QuadFmDemod);
 };
 
-class Int8ToFloat final : public BaseFilter {
+class Int8ToFloat final : public BaseFilter, public IGraphStepState {
  public:
+  hipStream_t graphStream() const noexcept final { return mQueue->cudaStream(); }
+  bool graphState(uint64_t& h) const noexcept final {
+    foldWindowState(h);
+    return true;
+  }
   static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
@@ -118,8 +146,11 @@ class Int8ToFloat final : public BaseFilter {
 };
 
 // Infinite phase-continuous tone (cos for Float, exp(j phi) for FloatComplex).
-class CosineSource final : public BaseSource {
+class CosineSource final : public BaseSource, public IGraphStepState {
  public:
+  hipStream_t graphStream() const noexcept final { return mQueue->cudaStream(); }
+  bool graphState(uint64_t&) const noexcept final { return false; }  // the phase argument advances
+
   static Result<Source> create(bool complexOutput, float sampleRate, float frequency, ICudaCommandQueue* queue,
                                IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
@@ -136,8 +167,13 @@ class CosineSource final : public BaseSource {
   REF_COUNTED(CosineSource);
 };
 
-class HipMemcpyFilter final : public BaseFilter {
+class HipMemcpyFilter final : public BaseFilter, public IGraphStepState {
  public:
+  hipStream_t graphStream() const noexcept final { return mQueue->cudaStream(); }
+  bool graphState(uint64_t& h) const noexcept final {
+    foldWindowState(h);
+    return true;
+  }
   static Result<Filter> create(hipMemcpyKind kind, ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
@@ -146,8 +182,10 @@ class HipMemcpyFilter final : public BaseFilter {
 
  private:
   HipMemcpyFilter(IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices, IMemSet* memSet,
-                  IBufferCopier* copier, std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept;
+                  IBufferCopier* copier, ICudaCommandQueue* queue,
+                  std::vector<ImmutableRef<IBufferCopier>>&& outputCopiers) noexcept;
   ConstRef<IBufferCopier> mCopier;
+  ConstRef<ICudaCommandQueue> mQueue;
   REF_COUNTED(HipMemcpyFilter);
 };
 

@@ -38,7 +38,9 @@ def _L():
                 ("gsdrAmChainWaitSlot", [vp, sz], err),
                 ("gsdrAmChainReset", [vp], err),
                 ("gsdrAmChainResidentOutputCount", [vp, sz], sz),
-                ("gsdrAmChainStepResident", [vp, vp, sz, vp, psz], err)):
+                ("gsdrAmChainStepResident", [vp, vp, sz, vp, psz], err),
+                ("gsdrAmChainChunksOutputCount", [vp, sz], sz),
+                ("gsdrAmChainStepChunks", [vp, vp, sz, vp, psz], err)):
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
@@ -108,6 +110,25 @@ class AmChain:
         got = ctypes.c_size_t()
         check(_L().gsdrAmChainStepResident(self._h, iq.data_ptr(), n_chunks, out.data_ptr(), ctypes.byref(got)),
               "gsdrAmChainStepResident")
+        torch.cuda.current_stream(iq.device).wait_stream(self.torch_stream)
+        return got.value
+
+    def chunks_output_count(self, n_chunks: int) -> int:
+        return _L().gsdrAmChainChunksOutputCount(self._h, n_chunks)
+
+    def step_chunks(self, iq: torch.Tensor, n_chunks: int, out: torch.Tensor) -> int:
+        """n_chunks live-stream chunk steps (each copied through the staging window exactly as
+        step() does) as ONE cached graph launch; the audio of all of them lands contiguously in
+        out. Returns the audio count."""
+        if iq.dtype != torch.int8 or not iq.is_cuda or iq.numel() < 2 * self.chunk * n_chunks:
+            raise ValueError("iq must be a device int8 tensor of n_chunks chunks")
+        n = self.chunks_output_count(n_chunks)
+        if out.numel() < n:
+            raise ValueError("out too small")
+        self.torch_stream.wait_stream(torch.cuda.current_stream(iq.device))
+        got = ctypes.c_size_t()
+        check(_L().gsdrAmChainStepChunks(self._h, iq.data_ptr(), n_chunks, out.data_ptr(), ctypes.byref(got)),
+              "gsdrAmChainStepChunks")
         torch.cuda.current_stream(iq.device).wait_stream(self.torch_stream)
         return got.value
 

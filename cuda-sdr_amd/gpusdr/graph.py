@@ -63,6 +63,8 @@ def _L():
             "gspDriverConnect": ([h, h, sz, h, sz], u32),
             "gspDriverSetupNode": ([h, h, ctypes.c_char_p], u32),
             "gspDriverDoFilter": ([h], u32),
+            "gspDriverDoFilterGraphed": ([h, h], u32),
+            "gspDriverGraphStats": ([h, psz, psz, psz], u32),
             "gspDriverNodeName": ([h, h, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int32)], sz),
         }
         for name, (args, res) in sigs.items():
@@ -261,3 +263,13 @@ class SteppingDriver(_Handle):
 
     def do_filter(self):
         _check(_L().gspDriverDoFilter(self._h), "doFilter")
+
+    def do_filter_graphed(self, queue: Queue):
+        """One step with its device work replayed from a hipGraph captured per repeating chain
+        state (gspDriverDoFilterGraphed); a plain step when the chain cannot be replayed."""
+        _check(_L().gspDriverDoFilterGraphed(self._h, queue.handle), "doFilterGraphed")
+
+    def graph_stats(self):
+        e, c, r = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        _check(_L().gspDriverGraphStats(self._h, ctypes.byref(e), ctypes.byref(c), ctypes.byref(r)), "graphStats")
+        return {"eager": e.value, "captured": c.value, "replayed": r.value}

@@ -42,6 +42,10 @@ class GS_PUBLIC BaseSink : public virtual Sink {
    * used bytes stay addressable through getPortInputBuffer()->readPtr()). */
   [[nodiscard]] Status consumeInputBytesAndMoveUsedToStart(size_t port, size_t numBytes) noexcept;
 
+  /* MI355X extension (graph stepping, driver.h): folds every input window's placement (base
+   * address, used range, capacity, checkout flag) into h. Non-virtual: no vtable change. */
+  void foldWindowState(uint64_t& h) const noexcept;
+
  private:
   const size_t mInputPortCount;
   ConstRef<IBufferSliceFactory> mSlicedBufferFactory;

@@ -90,6 +90,11 @@ GSP_API uint32_t gspDriverConnect(gspHandle driver, gspHandle source, size_t sou
                                   size_t sinkPort);
 GSP_API uint32_t gspDriverSetupNode(gspHandle driver, gspHandle node, const char* name);
 GSP_API uint32_t gspDriverDoFilter(gspHandle driver);
+/* MI355X extension: one doFilter step whose device work is replayed from a hipGraph captured per
+ * repeating chain state (every node a hot-path filter on `queue`'s stream; otherwise a plain step).
+ * gspDriverGraphStats counts plain, capturing and replayed steps. */
+GSP_API uint32_t gspDriverDoFilterGraphed(gspHandle driver, gspHandle queue);
+GSP_API uint32_t gspDriverGraphStats(gspHandle driver, size_t* eager, size_t* captured, size_t* replayed);
 /* Name given to `node` by setupNode (this driver or a nested one); *found = 0 if none. Returns the
  * name length; at most nameBufLen bytes are written (NUL-terminated when it fits). */
 GSP_API size_t gspDriverNodeName(gspHandle driver, gspHandle node, char* name, size_t nameBufLen, int32_t* found);

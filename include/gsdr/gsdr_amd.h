@@ -168,6 +168,13 @@ GSDR_API size_t gsdrAmChainNextOutputCount(gsdrAmChain chain);
 /* One step from device memory: chunkSamples IQ pairs at inputIq (copied into the staging window),
  * audio written to `output` (device, gsdrAmChainNextOutputCount floats). Asynchronous. */
 GSDR_API hipError_t gsdrAmChainStep(gsdrAmChain chain, const int8_t* inputIq, float* output, size_t* outputCount);
+/* nChunks consecutive chunk steps in ONE launch: the chunks are contiguous at inputIq (device),
+ * each is copied into the staging window and stepped exactly as gsdrAmChainStep does, and the audio
+ * of all of them is written contiguously at `output` (gsdrAmChainChunksOutputCount floats). The
+ * whole sequence is one graph, cached for the last (inputIq, nChunks, output, step parity). */
+GSDR_API size_t gsdrAmChainChunksOutputCount(gsdrAmChain chain, size_t nChunks);
+GSDR_API hipError_t gsdrAmChainStepChunks(gsdrAmChain chain, const int8_t* inputIq, size_t nChunks, float* output,
+                                          size_t* outputCount);
 /* Pinned ring. Fill input slot k (chunkSamples IQ pairs), call StepHost(k); after WaitSlot(k) the
  * output slot k holds *outputCount audio samples. A slot may be refilled after its WaitSlot. */
 GSDR_API int8_t* gsdrAmChainHostInputSlot(gsdrAmChain chain, size_t slot);

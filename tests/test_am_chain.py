@@ -128,3 +128,31 @@ def test_am_chain_resident_stream(chain_mod, orc):
     assert np.all(np.abs(got - want) <= bound)
     assert np.all(np.abs(ref - want) <= bound)
     assert np.all(np.abs(got - ref) <= 2 * bound)
+
+
+@pytest.mark.gpu
+def test_am_chain_multi_chunk_graph_matches_steps(chain_mod, orc):
+    """gsdrAmChainStepChunks (n chunk steps as one cached graph) gives exactly the per-chunk
+    steps' output, from the first step and from either staging parity, and meets the oracle."""
+    import torch
+    T, D, Ta, Da, L = 1023, 10, 255, 20, 4000
+    rng = np.random.default_rng(13)
+    rf = orc.lowpass_taps(T, 0.04)
+    au = orc.lowpass_taps(Ta, 0.02)
+    plan = [3, 2, 3, 3]  # parities 0/1 at the start of each batch, the cached graph reused
+    total = sum(plan)
+    iq = rng.integers(-128, 128, size=2 * L * total).astype(np.int8)
+    dev = torch.from_numpy(iq).cuda()
+    multi = chain_mod.AmChain(rf, D, au, Da, L)
+    got, pos = [], 0
+    for n in plan:
+        out = torch.empty(multi.chunks_output_count(n), dtype=torch.float32, device="cuda")
+        cnt = multi.step_chunks(dev[2 * L * pos:], n, out)
+        got.append(out[:cnt].cpu().numpy())
+        pos += n
+    got = np.concatenate(got)
+    per = chain_mod.AmChain(rf, D, au, Da, L)
+    ref = np.concatenate([per.step(dev[2 * L * s: 2 * L * (s + 1)]).cpu().numpy() for s in range(total)])
+    assert got.tobytes() == ref.tobytes()
+    want, bound = _expected(orc, iq, rf, D, au, Da)
+    assert np.all(np.abs(got - want) <= bound)

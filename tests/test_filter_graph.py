@@ -272,3 +272,80 @@ def test_frequency_shifter_fm_chain(graph, queue, orc):
     err = np.abs(got - want) / g
     assert np.median(err) <= 1e-3
     assert np.max(err) <= 5e-2, (int(np.argmax(err)), float(np.max(err)))
+
+
+def _am_chain_graph(graph, queue, taps, D):
+    """int8 IQ -> Int8ToFloat -> Fir -> QuadAmDemod -> HipMemcpy (device -> host), all on one queue;
+    the D2H filter is the graph tail the driver pulls through."""
+    conv = graph.Node.int8_to_float(queue)
+    fir = graph.Node.fir(queue, taps, D, graph.SAMPLE_FLOAT_COMPLEX)
+    am = graph.Node.quad_am_demod(queue)
+    d2h = graph.Node.from_json("HipMemcpy", '{"commandQueue": "qg", "from": "device", "to": "host"}', queue)
+    drv = graph.SteppingDriver()
+    drv.connect(conv, 0, fir, 0)
+    drv.connect(fir, 0, am, 0)
+    drv.connect(am, 0, d2h, 0)
+    return conv, d2h, drv
+
+
+def test_graph_stepping_matches_eager(graph, orc):
+    """SteppingDriver steps of an int8 -> cf32 -> FIR -> AM chain fed fixed-size chunks: the
+    graph-stepped driver (device work of each repeating chain state captured once, then replayed)
+    gives the eager driver's output bit for bit, and most steps are replays."""
+    queue = graph.Queue.named("qg")
+    T, D, chunk, steps = 127, 2, 6000, 40
+    taps = orc.lowpass_taps(T, 0.2)
+    rng = np.random.default_rng(21)
+    iq = rng.integers(-128, 128, size=2 * chunk * steps).astype(np.int8)
+    outs = {}
+    for mode in ("eager", "graphed"):
+        conv, tail, drv = _am_chain_graph(graph, queue, taps, D)
+        got = []
+        for s in range(steps):
+            conv.push(iq[2 * chunk * s: 2 * chunk * (s + 1)])
+            drv.do_filter() if mode == "eager" else drv.do_filter_graphed(queue)
+            got.append(_read_host(graph, queue, tail))
+        outs[mode] = np.concatenate(got)
+        if mode == "graphed":
+            st = drv.graph_stats()
+            assert st["replayed"] >= steps // 2 and st["captured"] >= 1, st
+    assert outs["graphed"].tobytes() == outs["eager"].tobytes()
+    x = orc.int8_to_float(iq).view(np.complex64)
+    y64, bound = orc.fir_f64(taps, x, D, len(outs["eager"]))
+    assert len(outs["eager"]) >= (chunk * steps - T) // D - chunk
+    assert np.all(np.abs(outs["eager"] - np.abs(y64)) <= FIR_TOL * bound + 1e-30)
+
+
+def _read_host(graph, queue, node):
+    size, _ = node.output_size()
+    if size == 0:
+        return np.zeros(0, np.float32)
+    buf = graph.Buffer.create_host(queue, size)
+    sl = buf.slice(0, size)
+    sl.clear()
+    node.read([sl])
+    return sl.to_host(np.float32)
+
+
+def test_graph_stepping_falls_back_for_a_tone_source(graph, orc):
+    """A chain with a CosineSource (its phase argument advances every step) is not replayable:
+    every step runs plainly and the output equals the eager driver's."""
+    queue = graph.Queue.named("qg")
+    outs = {}
+    for mode in ("eager", "graphed"):
+        src = graph.Node.cosine(queue, graph.SAMPLE_FLOAT_COMPLEX, 48000.0, 1000.0)
+        am = graph.Node.quad_am_demod(queue)
+        d2h = graph.Node.from_json("HipMemcpy", '{"commandQueue": "qg", "from": "device", "to": "host"}', queue)
+        drv = graph.SteppingDriver()
+        drv.connect(src, 0, am, 0)
+        drv.connect(am, 0, d2h, 0)
+        got = []
+        for _ in range(6):
+            drv.do_filter() if mode == "eager" else drv.do_filter_graphed(queue)
+            got.append(_read_host(graph, queue, d2h))
+        outs[mode] = np.concatenate(got)
+        if mode == "graphed":
+            st = drv.graph_stats()
+            assert st["captured"] == 0 and st["replayed"] == 0 and st["eager"] == 6, st
+    assert outs["graphed"].tobytes() == outs["eager"].tobytes()
+    assert len(outs["eager"]) > 0
