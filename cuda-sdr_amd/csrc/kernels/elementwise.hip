@@ -119,9 +119,7 @@ __global__ __launch_bounds__(kBlock) void quadFmDemod(const f2* __restrict__ in,
                                                       size_t n) {
   for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) {
     const f2 z0 = in[i], z1 = in[i + 1];
-    const float re = fmaf(z1.x, z0.x, z1.y * z0.y);
-    const float im = fmaf(z1.y, z0.x, -(z1.x * z0.y));
-    out[i] = gain * atan2f(im, re);
+    out[i] = fmDiscriminate(z0, z1, gain);
   }
 }
 

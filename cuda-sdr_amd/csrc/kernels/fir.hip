@@ -59,6 +59,7 @@ struct FirArgs {
   int32_t mix;         // complex input only: multiply sample n by exp(j theta(n)) first
   uint64_t mixPhase0;  // theta(n) = 2 pi (mixPhase0 + n mixStep) / 2^64: cycle fractions, so the
   uint64_t mixStep;    // phase wraps exactly (mod 2 pi) at any stream position
+  float fmGain;        // kEpiFm: discriminator gain
 };
 
 // Frequency shifter fused into the sample load (ComplexCosineSource x MultiplyCcc in
@@ -197,7 +198,9 @@ __global__ __launch_bounds__(kThreads) void firLdsKernel(FirArgs a) {
 
   const int64_t tile = xcdTile(blockIdx.x, gridDim.x);
   const int64_t tileOut = a.tileOutputs;
-  const int64_t k0 = tile * tileOut * (MODE == kFirFF ? 2 : 1);  // first output of the tile
+  // first FIR output of the tile; the FM epilogue needs y[k + 1] for output k, so its tiles
+  // overlap by one FIR output (tileOut - 1 discriminator outputs per tile)
+  const int64_t k0 = tile * (EPI == kEpiFm ? tileOut - 1 : tileOut) * (MODE == kFirFF ? 2 : 1);
   const int64_t inBase = k0 * a.D;
 
   // ---- stage the input window, phase-major -------------------------------------------
@@ -312,6 +315,17 @@ __global__ __launch_bounds__(kThreads) void firLdsKernel(FirArgs a) {
       float* o = reinterpret_cast<float*>(a.out);
       if (k < a.nOut) o[k] = amEnvelope(y0);
       if (k + 1 < a.nOut) o[k + 1] = amEnvelope(y1);
+    } else if (EPI == kEpiFm) {
+      // y[j + 2] (the next pair's first FIR output, summed over the tap slices in the same order)
+      f2 y2 = {0.0f, 0.0f};
+      if (j + 2 < tileOut) {
+        y2 = red[j + 2];
+#pragma unroll
+        for (int w = 1; w < WT; ++w) y2 += red[w * tileOut + j + 2];
+      }
+      float* o = reinterpret_cast<float*>(a.out);
+      if (j < tileOut - 1 && k < a.nOut) o[k] = fmDiscriminate(y0, y1, a.fmGain);
+      if (j + 1 < tileOut - 1 && k + 1 < a.nOut) o[k + 1] = fmDiscriminate(y1, y2, a.fmGain);
     } else {  // kEpiPair (FF): .x -> stream 0, .y -> stream 1 (tileOut further on)
       float* o = reinterpret_cast<float*>(a.out);
       const int64_t k2 = k + tileOut;
@@ -327,8 +341,11 @@ __global__ __launch_bounds__(kThreads) void firLdsKernel(FirArgs a) {
 // thread, taps and samples read through the caches.
 template <int MODE, int INK, int EPI>
 __global__ __launch_bounds__(kThreads) void firDirectKernel(FirArgs a) {
-  const int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (k >= a.nOut) return;
+  const int64_t k0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (k0 >= a.nOut) return;
+  f2 ys[2];
+  for (int u = 0; u < (EPI == kEpiFm ? 2 : 1); ++u) {  // FM: y[k] and y[k + 1]
+  const int64_t k = k0 + u;
   f2 acc = {0.0f, 0.0f}, tot = {0.0f, 0.0f};  // blocked sum, as in firLdsKernel
   const int64_t base = k * a.D;
   for (int j = 0; j < a.T; ++j) {
@@ -360,10 +377,16 @@ __global__ __launch_bounds__(kThreads) void firDirectKernel(FirArgs a) {
     }
   }
   acc += tot;
+  ys[u] = acc;
+  }
+  const int64_t k = k0;
+  const f2 acc = ys[0];
   if (EPI == kEpiComplex) {
     reinterpret_cast<f2*>(a.out)[k] = acc;
   } else if (EPI == kEpiAm) {
     reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc);
+  } else if (EPI == kEpiFm) {
+    reinterpret_cast<float*>(a.out)[k] = fmDiscriminate(ys[0], ys[1], a.fmGain);
   } else {
     reinterpret_cast<float*>(a.out)[k] = acc.x;  // FF direct: both lanes hold the same value
   }
@@ -523,7 +546,7 @@ hipError_t ensureLds(K kernel, size_t bytes) {
 
 template <int MODE, int INK, int EPI, int WO>
 hipError_t launchLds(FirArgs a, size_t lds, hipStream_t stream) {
-  const int64_t perTile = (int64_t)a.tileOutputs * (MODE == kFirFF ? 2 : 1);
+  const int64_t perTile = (EPI == kEpiFm ? a.tileOutputs - 1 : a.tileOutputs) * (MODE == kFirFF ? 2 : 1);
   const int64_t tiles = (a.nOut + perTile - 1) / perTile;
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
   auto kernel = firLdsKernel<MODE, INK, EPI, WO>;
@@ -574,7 +597,7 @@ struct MixSpec {
 
 template <int MODE, int INK, int EPI>
 hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t decimation, void* out,
-                     size_t nOut, int32_t device, hipStream_t stream, MixSpec mix = MixSpec{}) {
+                     size_t nOut, int32_t device, hipStream_t stream, MixSpec mix = MixSpec{}, float fmGain = 0.0f) {
   if (nOut == 0) return hipSuccess;
   if (in == nullptr || taps == nullptr || out == nullptr || tapCount == 0) return hipErrorInvalidValue;
   if (tapCount > 0x7fffffff || decimation > 0x7fffffff) return hipErrorInvalidValue;
@@ -582,13 +605,13 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
   if (!push.ok) return hipErrorInvalidDevice;
 
   // long real-tap filters on cf32 / int8 IQ: FFT fast convolution (HBM-bound; fir_fft.hip)
-  if constexpr (MODE == kFirFC && (INK == kInI8IQ || INK == kInCF32) && EPI != kEpiPair) if (!mix.on) {
+  if constexpr (MODE == kFirFC && (INK == kInI8IQ || INK == kInCF32) && EPI != kEpiPair && EPI != kEpiFm) if (!mix.on) {
     if ((kernelPolicy() & (GSDR_POLICY_NO_FFT | GSDR_POLICY_NO_MFMA)) == 0 && firFftEligible(tapCount, decimation, in, INK == kInI8IQ))
       return launchFirFft(in, INK == kInI8IQ, taps, tapCount, decimation, out, nOut, EPI, stream);
   }
   // int8 IQ with real taps: the exact int8 MFMA kernel when the shape allows it (the matrix-core
   // kernels take unmixed samples: a mixed stream is no longer integer)
-  if constexpr (MODE == kFirFC && INK == kInI8IQ && EPI != kEpiPair) if (!mix.on) {
+  if constexpr (MODE == kFirFC && INK == kInI8IQ && EPI != kEpiPair && EPI != kEpiFm) if (!mix.on) {
     if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firI8MfmaEligible(tapCount, decimation, in))
       return launchFirI8Mfma(static_cast<const int8_t*>(in), taps, tapCount, out, nOut, EPI, stream);
     // decimating / long filters: the split-K Toeplitz kernel on f16 planes
@@ -596,7 +619,7 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
       return launchFirI8DecMfma(static_cast<const int8_t*>(in), taps, tapCount, decimation, out, nOut, EPI, stream);
   }
   // cf32 with real taps: the split-precision bf16 MFMA kernel for the long-filter shapes
-  if constexpr (MODE == kFirFC && INK == kInCF32 && EPI != kEpiPair) if (!mix.on) {
+  if constexpr (MODE == kFirFC && INK == kInCF32 && EPI != kEpiPair && EPI != kEpiFm) if (!mix.on) {
     if ((kernelPolicy() & GSDR_POLICY_NO_MFMA) == 0 && firCfMfmaEligible(tapCount, decimation, in))
       return launchFirCfMfma(static_cast<const float*>(in), taps, tapCount, decimation, out, nOut, EPI, stream);
   }
@@ -607,7 +630,9 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
   a.taps = taps;
   a.out = out;
   a.nOut = (int64_t)nOut;
-  a.nIn = (int64_t)(nOut - 1) * (int64_t)s.decimation + (int64_t)tapCount;
+  // FM: nOut discriminator outputs read nOut + 1 FIR outputs
+  a.nIn = (int64_t)(EPI == kEpiFm ? nOut : nOut - 1) * (int64_t)s.decimation + (int64_t)tapCount;
+  a.fmGain = fmGain;
   a.T = (int32_t)tapCount;
   a.D = (int32_t)s.decimation;
   a.deff = (int32_t)s.deff;
@@ -634,7 +659,7 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
     // FF with many phases (the C5 audio FIR, D = 20): the phase-major staging of the LDS kernel
     // costs more than the taps; one output per thread over a shared window is faster
     const bool manyPhasesFF = MODE == kFirFF && s.decimation >= 8;
-    if ((tiles < 128 || manyPhasesFF) && lds <= kLdsSoftLimit) {
+    if (EPI != kEpiFm && (tiles < 128 || manyPhasesFF) && lds <= kLdsSoftLimit) {
       const int64_t blocks = ((int64_t)nOut + kThreads - 1) / kThreads;
       if constexpr (INK == kInCF32 || INK == kInI8IQ) {
         if (mix.on) {
@@ -791,6 +816,38 @@ hipError_t gsdrMixFirFCAmDemod(size_t decimation, const float* taps, size_t tapC
                                int32_t device, hipStream_t stream) {
   return launchFir<kFirFC, kInCF32, kEpiAm>(input, taps, tapCount, decimation, output, outputCount, device, stream,
                                             mixSpec(phase0, radiansPerSample));
+}
+
+hipError_t gsdrMixFirFCFmDemod(size_t decimation, const float* taps, size_t tapCount, const hipFloatComplex* input,
+                               double phase0, double radiansPerSample, float gain, float* output, size_t outputCount,
+                               int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInCF32, kEpiFm>(input, taps, tapCount, decimation, output, outputCount, device, stream,
+                                            mixSpec(phase0, radiansPerSample), gain);
+}
+
+hipError_t gsdrInt8MixFirFCFmDemod(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
+                                   double phase0, double radiansPerSample, float gain, float* output,
+                                   size_t outputCount, int32_t device, hipStream_t stream) {
+  return launchFir<kFirFC, kInI8IQ, kEpiFm>(inputIq, taps, tapCount, decimation, output, outputCount, device, stream,
+                                            mixSpec(phase0, radiansPerSample), gain);
+}
+
+// The reference's fused FM front (call site src/applications/fm_simpletest.cpp:400-413): shift the
+// channel to DC, low-pass + decimate, discriminate. Sample n of `input` is stream sample
+// firstSampleOffset + n (the reference passes the received count modulo the sample rate, so the
+// tone's phase restarts every second of signal - whole cycles when the offset frequency is a whole
+// number of Hz). Gain as QuadDemodFactory.h:108-110 at the discriminator's rate rfSampleRate / D.
+hipError_t gsdrFmDemod(size_t rfSampleRate, float tunedFrequency, float channelFrequency, float channelFmDeviation,
+                       size_t rfLowPassDecimation, size_t firstSampleOffset, const float* taps, size_t tapCount,
+                       const hipFloatComplex* input, float* output, size_t outputCount, int32_t device,
+                       hipStream_t stream) {
+  if (rfSampleRate == 0 || channelFmDeviation == 0.0f) return hipErrorInvalidValue;
+  const size_t D = rfLowPassDecimation < 1 ? 1 : rfLowPassDecimation;
+  const float demodRate = (float)rfSampleRate / (float)D;
+  const float gain = demodRate / (2.0f * (float)M_PI * channelFmDeviation * 5);
+  const double step = 2.0 * M_PI * ((double)tunedFrequency - (double)channelFrequency) / (double)rfSampleRate;
+  return gsdrMixFirFCFmDemod(D, taps, tapCount, input, step * (double)firstSampleOffset, step, gain, output,
+                             outputCount, device, stream);
 }
 
 hipError_t gsdrInt8MixFirFC(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,

@@ -6,7 +6,7 @@
 namespace gsdr_amd {
 
 enum FirMode : int { kFirFF = 0, kFirFC = 1, kFirCC = 2, kFirCF = 3 };
-enum FirEpilogue : int { kEpiComplex = 0, kEpiPair = 1, kEpiAm = 2 };
+enum FirEpilogue : int { kEpiComplex = 0, kEpiPair = 1, kEpiAm = 2, kEpiFm = 3 };
 
 struct FirPlanShape {
   size_t decimation;        // clamped to >= 1

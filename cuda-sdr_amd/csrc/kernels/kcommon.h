@@ -18,6 +18,13 @@ __device__ __forceinline__ float int8ToNorm(int8_t v) { return fmaxf(-1.0f, (flo
 // AM envelope (include/gsdr/gsdr.h, gsdrQuadAmDemod).
 __device__ __forceinline__ float amEnvelope(f2 z) { return sqrtf(fmaf(z.x, z.x, z.y * z.y)); }
 
+// FM discriminator (gsdrQuadFmDemod, QuadFmDemod.cpp:80-115): gain * arg(z1 conj(z0)).
+__device__ __forceinline__ float fmDiscriminate(f2 z0, f2 z1, float gain) {
+  const float re = fmaf(z1.x, z0.x, z1.y * z0.y);
+  const float im = fmaf(z1.y, z0.x, -(z1.x * z0.y));
+  return gain * atan2f(im, re);
+}
+
 // Map a launch-order block index to a tile so that tiles t and t+1 run on the same XCD
 // (blocks b and b+8 share an XCD under round-robin dispatch). Bijective for any grid size;
 // only affects L2 locality of the (taps-1) input halo, never correctness.

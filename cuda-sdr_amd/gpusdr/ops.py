@@ -265,3 +265,38 @@ def ws_aborts(device: int = 0, reset: bool = True) -> int:
     v = ctypes.c_uint64()
     check(L.gsdrAmdWsAborts(device, ctypes.byref(v), 1 if reset else 0), "gsdrAmdWsAborts")
     return int(v.value)
+
+
+def fm_front(taps: torch.Tensor, x: torch.Tensor, decimation: int, num_outputs: int, phase0: float,
+             radians_per_sample: float, gain: float, int8_iq: bool = False,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+    """Fused FM front (gsdrMixFirFCFmDemod / gsdrInt8MixFirFCFmDemod): mix, low-pass + decimate,
+    discriminate in one kernel. Needs num_outputs * D + T input samples."""
+    _require(taps, torch.float32, "taps")
+    _require(x, torch.int8 if int8_iq else torch.complex64, "x")
+    n_in = x.numel() // 2 if int8_iq else x.numel()
+    d = max(1, int(decimation))
+    if num_outputs > 0 and num_outputs * d + taps.numel() > n_in:
+        raise ValueError("input too short for the requested outputs")
+    if out is None:
+        out = torch.empty(num_outputs, dtype=torch.float32, device=x.device)
+    fn = lib().gsdrInt8MixFirFCFmDemod if int8_iq else lib().gsdrMixFirFCFmDemod
+    fn.argtypes = [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_double,
+                   ctypes.c_double, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_void_p]
+    check(fn(d, taps.data_ptr(), taps.numel(), x.data_ptr(), float(phase0), float(radians_per_sample), float(gain),
+             out.data_ptr(), num_outputs, _dev(x), _stream(x)), fn.__name__)
+    return out
+
+
+def fm_demod(rf_sample_rate: int, tuned: float, channel: float, deviation: float, decimation: int,
+             first_sample_offset: int, taps: torch.Tensor, x: torch.Tensor, num_outputs: int) -> torch.Tensor:
+    """The reference's gsdrFmDemod (fm_simpletest.cpp:400-413 call site)."""
+    out = torch.empty(num_outputs, dtype=torch.float32, device=x.device)
+    fn = lib().gsdrFmDemod
+    fn.argtypes = [ctypes.c_size_t, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_size_t, ctypes.c_size_t,
+                   ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                   ctypes.c_int32, ctypes.c_void_p]
+    check(fn(int(rf_sample_rate), float(tuned), float(channel), float(deviation), int(decimation),
+             int(first_sample_offset), taps.data_ptr(), taps.numel(), x.data_ptr(), out.data_ptr(), num_outputs,
+             _dev(x), _stream(x)), "gsdrFmDemod")
+    return out

@@ -70,6 +70,34 @@ GSDR_API hipError_t gsdrInt8MixFirFCAmDemod(size_t decimation, const float* taps
                                             float* output, size_t outputCount, int32_t device, hipStream_t stream);
 
 /*
+ * Fused FM front: frequency shift (as gsdrMixFirFC) -> low-pass FIR, decimate ->
+ * FM discriminator (the gsdrQuadFmDemod expression gain * arg(y[k+1] conj(y[k]))) in one kernel:
+ * output k uses FIR outputs k and k + 1, so the caller supplies outputCount * decimation + tapCount
+ * input samples (outputCount + 1 FIR outputs). A streaming caller carries the last FIR output's
+ * window like any FIR (consume outputCount * decimation samples); the discriminator's "previous
+ * sample" is the recomputed FIR output k, so nothing else is carried. Equals gsdrMixFirFC followed
+ * by gsdrQuadFmDemod bit for bit.
+ */
+GSDR_API hipError_t gsdrMixFirFCFmDemod(size_t decimation, const float* taps, size_t tapCount,
+                                        const hipFloatComplex* input, double phase0, double radiansPerSample,
+                                        float gain, float* output, size_t outputCount, int32_t device,
+                                        hipStream_t stream);
+GSDR_API hipError_t gsdrInt8MixFirFCFmDemod(size_t decimation, const float* taps, size_t tapCount,
+                                            const int8_t* inputIq, double phase0, double radiansPerSample, float gain,
+                                            float* output, size_t outputCount, int32_t device, hipStream_t stream);
+/*
+ * The reference's fused FM front gsdrFmDemod (call site src/applications/fm_simpletest.cpp:400-413;
+ * gsdr itself is not vendored, so argument types follow that call site): sample n of `input` is
+ * mixed by exp(j 2 pi (tuned - channel) (firstSampleOffset + n) / rfSampleRate), low-passed and
+ * decimated by rfLowPassDecimation, and discriminated with the QuadDemodFactory gain
+ * (rfSampleRate / D) / (2 pi channelFmDeviation 5) (QuadDemodFactory.h:108-110).
+ */
+GSDR_API hipError_t gsdrFmDemod(size_t rfSampleRate, float tunedFrequency, float channelFrequency,
+                                float channelFmDeviation, size_t rfLowPassDecimation, size_t firstSampleOffset,
+                                const float* taps, size_t tapCount, const hipFloatComplex* input, float* output,
+                                size_t outputCount, int32_t device, hipStream_t stream);
+
+/*
  * Deterministic synthetic sources for the benchmark configurations.
  * Sample n (absolute stream index firstSample + i) depends only on (seed, n), so a
  * time-sharded stream is generated shard by shard with no communication.

@@ -601,3 +601,56 @@ def test_fused_frequency_shift_fir(ops, orc, kind, T, D, n_out):
         y2 = _host(ops.fir(td, xd[w * h * D:], D, n_out - h, int8_iq=(kind == "i8"),
                            mix=(np.fmod(phase0 + h * D * step, 2 * np.pi), step)))
         _check_fir(np.concatenate([y1, y2]), y64, bound, ("mix-stream", kind, T, D))
+
+
+@pytest.mark.parametrize("kind,T,D,n_out", [("c64", 127, 4, 300_000), ("c64", 1023, 10, 30_000), ("i8", 255, 8, 40_000),
+                                             ("c64", 20000, 10, 300)])
+def test_fused_fm_front(ops, orc, kind, T, D, n_out):
+    """Mixer -> low-pass, decimate -> FM discriminator in ONE kernel (gsdr*MixFirFCFmDemod): bit-exact
+    against gsdrMixFirFC followed by gsdrQuadFmDemod where both run the LDS kernel (the first case,
+    enough tiles; the direct-kernel case too), and within the FIR tolerance carried through the
+    discriminator against the float64 oracle: |d arg| <= |dy_k|/|y_k| + |dy_k+1|/|y_k+1|."""
+    rng = np.random.default_rng(T * 7 + D)
+    n_in = n_out * D + T
+    phase0, step = 0.4, 2 * np.pi * 0.03
+    gain = orc.fm_gain(48000.0, 5000.0)
+    taps = orc.lowpass_taps(T, 0.3 / D)
+    if kind == "c64":
+        i = np.arange(n_in)
+        x = (np.exp(1j * (-step * i + 3.0 * np.sin(2 * np.pi * 1e-4 * i)))
+             + 0.05 * (rng.standard_normal(n_in) + 1j * rng.standard_normal(n_in))).astype(np.complex64)
+        xd, xf = _dev(x), x
+    else:
+        iq = rng.integers(-128, 128, size=2 * n_in).astype(np.int8)
+        xd, xf = _dev(iq), orc.int8_to_float(iq).view(np.complex64)
+    td = _dev(taps)
+    fm = _host(ops.fm_front(td, xd, D, n_out, phase0, step, gain, int8_iq=(kind == "i8")))
+    y = ops.fir(td, xd, D, n_out + 1, int8_iq=(kind == "i8"), mix=(phase0, step))
+    unfused = _host(ops.quad_fm_demod(y, gain))
+    if kind == "c64" and (n_out >= 100_000 or T > 10_000):
+        assert fm.tobytes() == unfused.tobytes()
+    mixed = orc.mix_f64(xf, phase0, step)
+    y64, bound = orc.fir_f64(taps, mixed.astype(np.complex64), D, n_out + 1)
+    want = gain * np.angle(y64[1:] * np.conj(y64[:-1]))
+    rel = FIR_TOL * bound / np.maximum(np.abs(y64), 1e-30)
+    tol = abs(gain) * (rel[:-1] + rel[1:] + 4e-7) + 1e-30
+    d = np.abs(fm - want)
+    d = np.minimum(d, np.abs(d - 2 * np.pi * abs(gain)))  # a branch-cut flip of arg near +-pi
+    assert np.all(d <= tol), (kind, T, D, float(np.max(d / tol)))
+
+
+def test_fm_demod_reference_entry(ops, orc):
+    """gsdrFmDemod, the reference's call (fm_simpletest.cpp:400-413): stream offset, channel shift
+    and QuadDemodFactory gain at the discriminator's rate, equal to the generic fused entry."""
+    rf_rate, tuned, channel, dev_hz, D, first = 4_800_000, 97.5e6, 98.5e6, 75e3, 10, 123_456
+    T, n_out = 255, 20_000
+    taps = orc.lowpass_taps(T, 0.04)
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal(n_out * D + T) + 1j * rng.standard_normal(n_out * D + T)).astype(np.complex64)
+    xd, td = _dev(x), _dev(taps)
+    got = _host(ops.fm_demod(rf_rate, tuned, channel, dev_hz, D, first, td, xd, n_out))
+    f32 = np.float32
+    step = 2 * np.pi * (float(f32(tuned)) - float(f32(channel))) / rf_rate
+    gain = float(f32(f32(rf_rate) / f32(D)) / (f32(2.0) * f32(np.pi) * f32(dev_hz) * f32(5)))
+    ref = _host(ops.fm_front(td, xd, D, n_out, step * first, step, gain))
+    assert got.tobytes() == ref.tobytes()
