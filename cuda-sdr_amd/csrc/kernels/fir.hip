@@ -31,6 +31,7 @@
 #include <atomic>
 #include <cmath>
 #include <type_traits>
+#include <utility>
 
 namespace gsdr_amd {
 
@@ -517,6 +518,133 @@ __global__ __launch_bounds__(kThreads) void firSmallKernel(FirArgs a) {
   }
 }
 
+// Decimating real FIR (FF, even D >= 4, ceil(T / D) <= 32: the C5 audio filter, 255 taps, D = 20).
+// A 128-thread block owns 512 consecutive outputs; lane t owns 4 of them. The block's input window
+// is staged in LDS PHASE-PAIR-major: element (pp, m) is the float2 (x[m D + 2pp], x[m D + 2pp + 1]),
+// so one packed FMA advances two phases at once against the tap pair (h[q D + 2pp], h[q D + 2pp + 1]),
+// staged alongside (a wave-uniform LDS broadcast). Per phase pair a lane reads its R + QB - 1 element
+// window with ds_read_b128 (lanes 16 B apart: conflict free) and slides it over the taps in
+// registers: 2 window reads per 8 packed FMAs (firSmallKernel: 2 LDS reads per FMA).
+// Sum order: per phase, ceil(T / D) taps in sequence; then the phase partials in order (the
+// same bound as firSmallKernel's; tests hold both against float64).
+constexpr int kDecR = 4;
+constexpr int kDecThreads = 128;
+constexpr int kDecOut = kDecR * kDecThreads;
+constexpr int kDecLoads = 8;   // float4 staging loads in flight per lane
+constexpr int kDecMaxQ = 32;   // taps per phase
+
+// Per-phase-pair LDS: the window rows (even count: 16 B aligned rows) and the tap pairs (even count)
+__host__ __device__ constexpr int decRows(int QM) { return kDecOut + QM + (QM & 1) + 2; }
+__host__ __device__ constexpr int decTapRows(int QM) { return QM + (QM & 1); }
+__host__ __device__ inline size_t decLdsBytes(int QM, int D) {
+  return (size_t)(D / 2) * (size_t)(decRows(QM) + decTapRows(QM)) * 8;
+}
+
+// QM = ceil(T / D) exactly: the tap loop is straight-line code over a register window
+template <int QM>
+__global__ __launch_bounds__(kDecThreads) void firDecFFKernel(FirArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int M = decRows(QM), MT = decTapRows(QM);
+  const int D = a.D, T = a.T, H = a.D >> 1;
+  f2* win = reinterpret_cast<f2*>(smem);
+  f2* tapsL = win + H * M;  // (pp, q) at pp MT + q: (h[q D + 2pp], h[q D + 2pp + 1]), zero past T
+  const int tid = threadIdx.x;
+  const int64_t k0 = (int64_t)blockIdx.x * kDecOut;
+  const int64_t base = k0 * D;  // float index; a multiple of 4 (kDecOut D, D even)
+  const int64_t avail = a.nIn - base;
+  for (int i = tid; i < H * MT; i += kDecThreads) {
+    const int pp = i / MT, q = i - pp * MT;
+    const int j = q * D + 2 * pp;
+    tapsL[i] = f2{j < T ? a.taps[j] : 0.0f, j + 1 < T ? a.taps[j + 1] : 0.0f};
+  }
+  // the window covers QM whole tap rows per output (the empty slots of the last row included), so
+  // every element the tap loop reads is staged: samples past the input are staged as zeros
+  const int span = (kDecOut - 1 + QM) * D;
+  const float* src = reinterpret_cast<const float*>(a.in) + base;
+  // staging: float4 = two phase pairs; kDecLoads loads in flight per lane, then the pair scatter
+  const int n4 = (span + 3) >> 2;
+  const float invH = 1.0f / (float)H;
+  for (int u0 = 0; u0 < n4; u0 += kDecLoads * kDecThreads) {
+    float4 v[kDecLoads];
+#pragma unroll
+    for (int u = 0; u < kDecLoads; ++u) {
+      const int i4 = u0 + u * kDecThreads + tid;
+      const int64_t f = (int64_t)i4 * 4;
+      if (i4 < n4 && f + 3 < avail) {
+        v[u] = reinterpret_cast<const float4*>(src)[i4];
+      } else {
+        v[u] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (i4 < n4) {
+          if (f < avail) v[u].x = src[f];
+          if (f + 1 < avail) v[u].y = src[f + 1];
+          if (f + 2 < avail) v[u].z = src[f + 2];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kDecLoads; ++u) {
+      const int i4 = u0 + u * kDecThreads + tid;
+      if (i4 >= n4) continue;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * i4 + h;  // pair index: samples 2j, 2j + 1
+        int m = (int)((float)j * invH);
+        m -= m * H > j ? 1 : 0;
+        m += (m + 1) * H <= j ? 1 : 0;
+        const int pp = j - m * H;
+        if (m < M) win[pp * M + m] = h ? f2{v[u].z, v[u].w} : f2{v[u].x, v[u].y};
+      }
+    }
+  }
+  __syncthreads();
+  f2 tot[kDecR];
+#pragma unroll
+  for (int r = 0; r < kDecR; ++r) tot[r] = f2{0.0f, 0.0f};
+  constexpr int kWin = kDecR + QM - 1 + ((kDecR + QM - 1) & 1);  // window elements, even
+  for (int pp = 0; pp < H; ++pp) {
+    const f4* row = reinterpret_cast<const f4*>(smem) + (pp * M + kDecR * tid) / 2;
+    const f4* hp = reinterpret_cast<const f4*>(tapsL) + pp * MT / 2;
+    f2 x[kWin], hq[MT];
+#pragma unroll
+    for (int i = 0; i < kWin / 2; ++i) {
+      const f4 w = row[i];
+      x[2 * i] = f2{w.x, w.y};
+      x[2 * i + 1] = f2{w.z, w.w};
+    }
+#pragma unroll
+    for (int i = 0; i < MT / 2; ++i) {
+      const f4 w = hp[i];
+      hq[2 * i] = f2{w.x, w.y};
+      hq[2 * i + 1] = f2{w.z, w.w};
+    }
+    f2 cur[kDecR];
+#pragma unroll
+    for (int r = 0; r < kDecR; ++r) cur[r] = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < QM - 1; ++q) {
+#pragma unroll
+      for (int r = 0; r < kDecR; ++r) cur[r] = __builtin_elementwise_fma(hq[q], x[r + q], cur[r]);
+    }
+    // the last tap row holds two, one or no taps of this phase pair: no product is formed past
+    // the last tap (a zero tap x inf would spread a NaN)
+    const int jLast = (QM - 1) * D + 2 * pp;
+    if (jLast + 1 < T) {
+#pragma unroll
+      for (int r = 0; r < kDecR; ++r) cur[r] = __builtin_elementwise_fma(hq[QM - 1], x[r + QM - 1], cur[r]);
+    } else if (jLast < T) {
+#pragma unroll
+      for (int r = 0; r < kDecR; ++r) cur[r].x = fmaf(hq[QM - 1].x, x[r + QM - 1].x, cur[r].x);
+    }
+#pragma unroll
+    for (int r = 0; r < kDecR; ++r) tot[r] += cur[r];
+  }
+  const int64_t k = k0 + kDecR * tid;
+  float* out = reinterpret_cast<float*>(a.out);
+#pragma unroll
+  for (int r = 0; r < kDecR; ++r)
+    if (k + r < a.nOut) out[k + r] = tot[r].x + tot[r].y;
+}
+
 // ---- host side --------------------------------------------------------------------------
 
 namespace {
@@ -595,6 +723,13 @@ struct MixSpec {
   uint64_t phase0 = 0, step = 0;
 };
 
+template <int... Q>
+void (*decFFTable(std::integer_sequence<int, Q...>, int qm))(FirArgs) {
+  static void (*const kTable[])(FirArgs) = {firDecFFKernel<Q + 1>...};
+  return kTable[qm - 1];
+}
+inline void (*decFFKernel(int qm))(FirArgs) { return decFFTable(std::make_integer_sequence<int, kDecMaxQ>{}, qm); }
+
 template <int MODE, int INK, int EPI>
 hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t decimation, void* out,
                      size_t nOut, int32_t device, hipStream_t stream, MixSpec mix = MixSpec{}, float fmGain = 0.0f) {
@@ -659,6 +794,20 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
     // FF with many phases (the C5 audio FIR, D = 20): the phase-major staging of the LDS kernel
     // costs more than the taps; one output per thread over a shared window is faster
     const bool manyPhasesFF = MODE == kFirFF && s.decimation >= 8;
+    if constexpr (MODE == kFirFF && INK == kInF32 && EPI == kEpiPair) {
+      // even D >= 4, up to 32 taps per phase: the phase-pair register-window kernel
+      const size_t D = s.decimation;
+      const size_t ldsDec = qmax <= (size_t)kDecMaxQ ? decLdsBytes((int)qmax, (int)D) : 0;
+      if ((tiles < 128 || manyPhasesFF) && D >= 4 && D % 2 == 0 && qmax <= (size_t)kDecMaxQ &&
+          ldsDec <= kLdsSoftLimit && (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
+        auto kernel = decFFKernel((int)qmax);
+        hipError_t e = ensureLds(kernel, ldsDec);
+        if (e != hipSuccess) return e;
+        const int64_t blocks = ((int64_t)nOut + kDecOut - 1) / kDecOut;
+        hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kDecThreads), ldsDec, stream, a);
+        return hipGetLastError();
+      }
+    }
     if (EPI != kEpiFm && (tiles < 128 || manyPhasesFF) && lds <= kLdsSoftLimit) {
       const int64_t blocks = ((int64_t)nOut + kThreads - 1) / kThreads;
       if constexpr (INK == kInCF32 || INK == kInI8IQ) {
