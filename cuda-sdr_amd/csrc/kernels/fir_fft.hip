@@ -62,7 +62,7 @@ __device__ unsigned long long gDirectBlocks;
 constexpr int kM = 512;       // FFT points per phase per block
 constexpr int kWaves = 8;     // waves per workgroup (one workgroup per CU)
 constexpr int kThreads = kWaves * kWave;
-constexpr int kStride = 9;    // exchange scratch row stride (complex): conflict-light b64 access
+constexpr int kSA = 10;       // pattern-A exchange row stride (complex): see exchangeA
 
 enum Input : int { kCf32 = 0, kI8 = 1 };
 enum Epi : int { kComplex = 0, kAm = 1 };
@@ -159,13 +159,16 @@ __device__ __forceinline__ void dft8(f2 (&z)[8]) {
   z[7] = b3 + t7 * sv;
 }
 
-// LDS layout (complex units): [G: D x 8 x 64][twiddles: 4 x 7 x 64][scratch: kWaves x scratch].
-// Twiddles are per-lane tables tw[s][r][l] (the four stage boundaries of the forward / inverse
-// 512-point DFT, r = 1..7), so every twiddle read is one base register + an immediate offset.
-constexpr int kTw = 4 * 7 * 64;
+// LDS layout (complex units): [G: D x 8 x 64][twiddles: 4 x 8 x 64][scratch: kWaves x scratch].
+// Every table is read 16 bytes per lane (ds_read_b128, lanes 16 B apart: conflict free, 256 B/clk;
+// two 8-byte reads would be fused by the compiler into ds_read2_b64 / ds_read2st64_b64 at half
+// that rate). G: f4 (G_p[d], G_p[d + 1]) at (p 4 + d / 2) 64 + l. Twiddles: per-lane tables for the
+// four stage boundaries of the forward / inverse 512-point DFT, f4 (t_k, t_k+1) at
+// (stage 4 + k / 2) 64 + l, t_k = W^(e r) with r = k + 1 = 1..7 (slot 7 unused).
+constexpr int kTw = 4 * 8 * 64;
 struct Lds {
-  f2* g;
-  const f2* tw;  // tw + l: this lane's column
+  f4* g;
+  const f4* tw;  // tw + l: this lane's column
   f2* scratch;   // this wave's
 };
 
@@ -175,31 +178,58 @@ struct Lds {
 // not reorder them (it reasons per lane and would move a read above a write it proves disjoint).
 __device__ __forceinline__ void ldsOrder() { asm volatile("" ::: "memory"); }
 
-// Digit transpose of NP independent columns through the wave's scratch (NP areas of kXch
-// complex): register r of column n goes to area n at base + r * step; then every lane reads its
-// row of 8 (stride kStride). The NP columns' writes and reads are issued back to back, so one
-// column's LDS latency overlaps the other's.
-constexpr int kXch = 64 * kStride;
+// Digit transposes of NP independent columns through the wave's scratch (NP areas of kXch
+// complex): register r of lane l = (a = l & 7, hi = l >> 3) is written to one row, then every lane
+// reads its own row of 8 (row l) as four 16-byte reads. The NP columns' writes and reads are
+// issued back to back, so one column's LDS latency overlaps the other's. Both layouts are
+// bank-conflict free for the 8-byte writes (16-lane groups, 32 banks) and the 16-byte reads
+// (ds_read_b128 lane groups, 64 banks) - MI355X_MICROARCH.md LDS table.
+//   pattern A: r -> row a + 8 r, col hi; rows kSA = 10 complex apart.
+//   pattern B: r -> row 8 hi + r, col a; rows 8 complex apart plus 8 after every 8th row, and
+//              the column pairs XOR-swizzled by row & 3: (row, col) at 9 row - row % 8 + (col ^ 2 (row & 3)).
+constexpr int kXch = 64 * kSA;  // >= pattern B's 72 x 8
 template <int NP>
-__device__ __forceinline__ void exchange(f2 (&z)[NP][8], f2* s, int l, int base, int step) {
+__device__ __forceinline__ void readRows(f2 (&z)[NP][8], const f2* s, int rowOff, int sw) {
 #pragma unroll
   for (int n = 0; n < NP; ++n)
 #pragma unroll
-    for (int r = 0; r < 8; ++r) s[n * kXch + base + r * step] = z[n][r];
+    for (int c = 0; c < 4; ++c) {
+      const f4 v = *reinterpret_cast<const f4*>(s + n * kXch + rowOff + ((2 * c) ^ sw));
+      z[n][2 * c] = f2{v.x, v.y};
+      z[n][2 * c + 1] = f2{v.z, v.w};
+    }
+}
+template <int NP>
+__device__ __forceinline__ void exchangeA(f2 (&z)[NP][8], f2* s, int l) {
+  const int a = l & 7, hi = l >> 3;
+#pragma unroll
+  for (int n = 0; n < NP; ++n)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) s[n * kXch + (a + 8 * r) * kSA + hi] = z[n][r];
   ldsOrder();
-#pragma unroll
-  for (int n = 0; n < NP; ++n)
-#pragma unroll
-    for (int r = 0; r < 8; ++r) z[n][r] = s[n * kXch + l * kStride + r];
+  readRows<NP>(z, s, l * kSA, 0);
   ldsOrder();
 }
-
-__device__ __forceinline__ f2 twiddle(const Lds& L, int stage, int r) { return L.tw[(stage * 7 + r - 1) * 64]; }
+template <int NP>
+__device__ __forceinline__ void exchangeB(f2 (&z)[NP][8], f2* s, int l) {
+  const int a = l & 7, hi = l >> 3;
+#pragma unroll
+  for (int n = 0; n < NP; ++n)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) s[n * kXch + 72 * hi + 8 * r + (a ^ (2 * (r & 3)))] = z[n][r];
+  ldsOrder();
+  readRows<NP>(z, s, 72 * hi + 8 * a, 2 * (l & 3));
+  ldsOrder();
+}
 
 template <int NP>
 __device__ __forceinline__ void loadTw(f2 (&t)[7], const Lds& L, int stage) {
 #pragma unroll
-  for (int r = 1; r < 8; ++r) t[r - 1] = twiddle(L, stage, r);
+  for (int kp = 0; kp < 4; ++kp) {
+    const f4 v = L.tw[(stage * 4 + kp) * 64];
+    t[2 * kp] = f2{v.x, v.y};
+    if (2 * kp + 1 < 7) t[2 * kp + 1] = f2{v.z, v.w};
+  }
 }
 
 template <int NP>
@@ -220,34 +250,32 @@ __device__ __forceinline__ void twiddleAll(f2 (&z)[NP][8], const f2 (&t)[7]) {
 // loaded a stage ahead (before the exchange that precedes their use) and shared by the columns.
 template <int NP>
 __device__ __forceinline__ void fftFwd(f2 (&z)[NP][8], const Lds& L, int l) {
-  const int a = l & 7, hi = l >> 3;
   f2 t[7];
   loadTw<NP>(t, L, 0);  // W512^(m1 k0), m1 = l
 #pragma unroll
   for (int n = 0; n < NP; ++n) dft8<false>(z[n]);  // over m2 -> k0
   twiddleAll<NP>(z, t);
   loadTw<NP>(t, L, 1);  // W64^(a c)
-  exchange<NP>(z, L.scratch, l, a * kStride + hi, 8 * kStride);  // -> lane 8 k0 + a, reg b
+  exchangeA<NP>(z, L.scratch, l);  // -> lane 8 k0 + a, reg b
 #pragma unroll
   for (int n = 0; n < NP; ++n) dft8<false>(z[n]);  // over b -> c
   twiddleAll<NP>(z, t);
-  exchange<NP>(z, L.scratch, l, 8 * hi * kStride + a, kStride);  // -> lane 8 k0 + c, reg a
+  exchangeB<NP>(z, L.scratch, l);  // -> lane 8 k0 + c, reg a
 #pragma unroll
   for (int n = 0; n < NP; ++n) dft8<false>(z[n]);  // over a -> d
 }
 
 // Inverse (unscaled) 512-point DFT from layout F: out lane L, z[h] = y[L + 64 h].
 __device__ __forceinline__ void ifft512(f2 (&zz)[1][8], const Lds& L, int l) {
-  const int lo = l & 7, hi = l >> 3;
   f2 t[7];
   loadTw<1>(t, L, 2);  // W512^-((k0 + 8 c) e)
   dft8<true>(zz[0]);   // over d -> e (lane 8 k0 + c)
   twiddleAll<1>(zz, t);
   loadTw<1>(t, L, 3);  // W64^-(k0 g)
-  exchange<1>(zz, L.scratch, l, 8 * hi * kStride + lo, kStride);  // -> lane 8 k0 + e, reg c
+  exchangeB<1>(zz, L.scratch, l);  // -> lane 8 k0 + e, reg c
   dft8<true>(zz[0]);   // over c -> g
   twiddleAll<1>(zz, t);
-  exchange<1>(zz, L.scratch, l, lo * kStride + hi, 8 * kStride);  // -> lane e + 8 g, reg k0
+  exchangeA<1>(zz, L.scratch, l);  // -> lane e + 8 g, reg k0
   dft8<true>(zz[0]);   // over k0 -> h
 }
 
@@ -258,7 +286,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t blockRsrc(const void* base, in
 
 template <int D>
 constexpr int scratchComplex(int input) {
-  // two exchange areas (2 x 64 x kStride) | cf32 row-group image (64 D) | int8 block image (512 D x 2 B + 16)
+  // two exchange areas (2 x kXch) | cf32 row-group image (64 D) | int8 block image (512 D x 2 B + 16)
   return input == kCf32 ? (64 * D > 2 * kXch ? 64 * D : 2 * kXch)
                         : ((1024 * D + 16) / 8 > 2 * kXch ? (1024 * D + 16 + 7) / 8 : 2 * kXch);
 }
@@ -272,7 +300,8 @@ constexpr size_t ldsBytes() {
 template <int D, int IN>
 __device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l) {
   for (int n = threadIdx.x; n < kTw; n += kThreads) {
-    const int lane = n & 63, r = (n >> 6) % 7 + 1, stage = n / (7 * 64);
+    // complex n = ((stage 4 + kp) 64 + lane) 2 + (k & 1), k = 2 kp + (n & 1), r = k + 1
+    const int stage = n >> 9, kp = (n >> 7) & 3, lane = (n >> 1) & 63, r = 2 * kp + (n & 1) + 1;
     const int lo = lane & 7, hi = lane >> 3;
     int e;  // exponent of W512 = exp(-2 pi i / 512)
     switch (stage) {
@@ -283,7 +312,7 @@ __device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l
     }
     double sn, cs;
     sincospi(-2.0 * e / kM, &sn, &cs);
-    twAll[n] = f2{(float)cs, (float)sn};
+    twAll[n] = r == 8 ? f2{0.0f, 0.0f} : f2{(float)cs, (float)sn};
   }
   __syncthreads();
   const float sc = a.inScale / (float)kM;
@@ -297,7 +326,8 @@ __device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l
     }
     fftFwd<1>(z, L, l);
 #pragma unroll
-    for (int d = 0; d < 8; ++d) L.g[(p * 8 + d) * 64 + l] = f2{z[0][d].x * sc, -z[0][d].y * sc};
+    for (int d = 0; d < 8; d += 2)
+      L.g[(p * 4 + d / 2) * 64 + l] = f4{z[0][d].x * sc, -z[0][d].y * sc, z[0][d + 1].x * sc, -z[0][d + 1].y * sc};
   }
   __syncthreads();
 }
@@ -365,7 +395,11 @@ __device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kCf32
     for (int i = 0; i < D / 2; ++i) s4[i * 64 + l] = f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
     ldsOrder();
 #pragma unroll
-    for (int p = 0; p < D; ++p) R.v[j][p] = s[l * D + p];
+    for (int p = 0; p < D; p += 2) {  // row l: 16-byte reads (D even), lanes 16 D bytes apart
+      const f4 u = reinterpret_cast<const f4*>(s)[(l * D + p) / 2];
+      R.v[j][p] = f2{u.x, u.y};
+      R.v[j][p + 1] = f2{u.z, u.w};
+    }
     ldsOrder();
   }
 }
@@ -489,12 +523,12 @@ __device__ void directBlock(const Args& a, int64_t b, int l) {
 
 template <int D, int IN, int EPI>
 __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
-  extern __shared__ f2 lds[];
+  extern __shared__ __attribute__((aligned(16))) f2 lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   f2* twAll = lds + D * 8 * 64;
   Lds L;
-  L.g = lds;
-  L.tw = twAll + l;
+  L.g = reinterpret_cast<f4*>(lds);
+  L.tw = reinterpret_cast<const f4*>(twAll) + l;
   L.scratch = twAll + kTw + w * scratchComplex<D>(IN);
   buildTables<D, IN>(a, twAll, L, w, l);
   if (w >= kWaves / 2) {
@@ -533,7 +567,11 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
       for (int n = 0; n < NP; ++n) {
         f2 g[8], u[8];
 #pragma unroll
-        for (int d = 0; d < 8; ++d) g[d] = L.g[((p + n) * 8 + d) * 64 + l];
+        for (int d = 0; d < 8; d += 2) {
+          const f4 v = L.g[((p + n) * 4 + d / 2) * 64 + l];
+          g[d] = f2{v.x, v.y};
+          g[d + 1] = f2{v.z, v.w};
+        }
 #pragma unroll
         for (int d = 0; d < 8; ++d) u[d] = cmac1(z[n][d], g[d], acc[0][d]);
 #pragma unroll

@@ -3,7 +3,7 @@
 #   bash tools/exp/run_fft_variants.sh build   # CPU container
 #   bash tools/exp/run_fft_variants.sh run     # GPU box
 # GSDR_FFT_EXP bits: 1 no FFT math, 2 no global loads, 4 no LDS transposition, 8 no guard,
-# 16 no stores.
+# 16 no stores. An optional third field names another source file (e.g. a saved baseline).
 set -eu
 cd "$(dirname "$0")/../.."
 OUT=tools/exp/_build_fft
@@ -22,11 +22,11 @@ load_only|-DGSDR_FFT_EXP=29"}
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
   decls=""; table=""; objs=""; i=0
-  while IFS='|' read -r name flags; do
+  while IFS='|' read -r name flags src; do
     [ -z "$name" ] && continue
     hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Iinclude -Icuda-sdr_amd/csrc/kernels \
       -Dgsdr_amd=f$i -DgsdrAmdSetFftGuard=f${i}_sg -DgsdrAmdGetFftGuard=f${i}_gg -DgsdrAmdFftDirectBlocks=f${i}_db \
-      $flags -c $KSRC -o $OUT/f$i.o &
+      $flags -c ${src:-$KSRC} -o $OUT/f$i.o &
     decls="$decls DECL($i)"; table="$table {\"$name\", f$i::launchFirFft},"; objs="$objs $OUT/f$i.o"
     i=$((i+1))
   done <<< "$VARIANTS"
