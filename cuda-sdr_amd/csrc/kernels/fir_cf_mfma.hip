@@ -47,10 +47,6 @@ typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
-#ifndef GSDR_CF_EXPERIMENT
-#define GSDR_CF_EXPERIMENT 0  // attribution builds only (tools/exp): 1 = skip split, 2 = skip MFMA,
-                              // 4 = skip loads, 8 = skip reduction/stores, 32 = clock stamps
-#endif
 constexpr int kCfWaves = 8;
 constexpr int kCfThreads = kCfWaves * kWave;
 constexpr int kCfTileOut = 512;  // 16 rows x 32 columns
@@ -240,7 +236,7 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
     v16f acc = v16f{};
 #pragma unroll
     for (int s = 0; s < kCfMaxKS; ++s) {
-      if (s < KS && !(GSDR_CF_EXPERIMENT & 2)) {
+      if (s < KS) {
         const int u = uRow + 2 * (wave * KS + s);
         const int off = 16 * cfPhys(u, a.padShift);
         const bf8 x0 = *reinterpret_cast<const bf8*>(pI + off);
@@ -254,10 +250,6 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, bf[s][0], acc, 0, 0, 0);
       }
     }
-    if (GSDR_CF_EXPERIMENT & 8) {
-      if (acc[0] + acc[7] + acc[13] == 1.2345f) reinterpret_cast<float*>(a.out)[lane] = 0.0f;
-      __syncthreads();
-    } else {
 #pragma unroll
     for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
     __syncthreads();  // partials complete; every wave is done reading the planes
@@ -276,12 +268,11 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
       else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq};
     }
     }
-    }
 
     // ---- next tile's window into the planes, the one after into registers ------------------
     if (i + 1 < n) {
-      if (!(GSDR_CF_EXPERIMENT & 1)) splitWindow<G>(a, win, planes, tid, &nonFinite[(tile + 1) & 1]);
-      if (i + 2 < n && !(GSDR_CF_EXPERIMENT & 4)) loadWindow<G>(a, tile + 2, tid, win);
+      splitWindow<G>(a, win, planes, tid, &nonFinite[(tile + 1) & 1]);
+      if (i + 2 < n) loadWindow<G>(a, tile + 2, tid, win);
       __syncthreads();
     }
   }
@@ -426,8 +417,8 @@ __device__ __forceinline__ void cfF16Tile(const CfFirArgs& a, int8_t* smem, floa
   const int tile = t0 + i;
   int8_t* cur = smem + (i & 1) * 4 * a.planeStride;
   int8_t* nxt = smem + ((i + 1) & 1) * 4 * a.planeStride;
-  if (i + 2 < n && !(GSDR_CF_EXPERIMENT & 4)) loadWindow<G>(a, tile + 2, tid, wNext);
-  const bool splitNext = i + 1 < n && !nx.direct && !(GSDR_CF_EXPERIMENT & 1);
+  if (i + 2 < n) loadWindow<G>(a, tile + 2, tid, wNext);
+  const bool splitNext = i + 1 < n && !nx.direct;
   const float scaleN = ldexpf(1.0f, nx.sx);
   if (st.direct) {
     directTile<EPI>(a, tile, tid);
@@ -445,34 +436,23 @@ __device__ __forceinline__ void cfF16Tile(const CfFirArgs& a, int8_t* smem, floa
         const int off = 16 * cfPhys(u, a.padShift);
         const h8 x0 = *reinterpret_cast<const h8*>(pI + off);
         const h8 x1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
-        if (GSDR_CF_EXPERIMENT & 2) {
-          acc[s] += (float)x0[0] + (float)x1[1];
-        } else {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
-        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
 #pragma unroll
         for (int j = 0; j < G; ++j)
           if (s == (KS * (j + 1)) / (G + 1) && splitNext) splitGroupF16<G>(a, wCur, nxt, tid, scaleN, j);
       }
     }
-    if (GSDR_CF_EXPERIMENT & 8) {
-      if (acc[0] + acc[7] + acc[13] == 1.2345f) reinterpret_cast<float*>(a.out)[lane] = 0.0f;
-    } else {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
-    }
+    for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
   }
   // tile i + 2's statistics (its loads had the MFMA phase to land); red2 alternates by tile
-  if (i + 2 < n && !(GSDR_CF_EXPERIMENT & 16)) cfStatsLocal<G>(a, wNext, tid, red2[i & 1]);
+  if (i + 2 < n) cfStatsLocal<G>(a, wNext, tid, red2[i & 1]);
   __syncthreads();  // partials and statistics published; `cur` read and `nxt` written by all waves
   CfF16State nn{0, true};
-  if (i + 2 < n) {
-    if (GSDR_CF_EXPERIMENT & 16) nn.direct = false;
-    else nn.direct = cfStatsFinish(red2[i & 1], &nn.sx);
-  }
-  if (!st.direct && !(GSDR_CF_EXPERIMENT & 8)) {
+  if (i + 2 < n) nn.direct = cfStatsFinish(red2[i & 1], &nn.sx);
+  if (!st.direct) {
     float yi = 0.0f, yq = 0.0f;
 #pragma unroll
     for (int v = 0; v < kCfWaves; ++v) {
@@ -679,15 +659,7 @@ __device__ __forceinline__ void wsSignal(int* p, int lane) {
   if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-#if GSDR_CF_EXPERIMENT & 32
-// attribution builds: per (block, wave) cycles spent in wsWait, and the wave's total cycles
-__device__ unsigned long long gWsStamp[256 * 16][2];
-#endif
-
 __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
-#if GSDR_CF_EXPERIMENT & 32
-  const uint64_t t0 = __builtin_amdgcn_s_memtime();
-#endif
   for (int it = 0;; ++it) {
     const int v = waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (v >= target) break;
@@ -703,10 +675,6 @@ __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
     __builtin_amdgcn_s_sleep(1);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#if GSDR_CF_EXPERIMENT & 32
-  if ((threadIdx.x & 63) == 0)
-    gWsStamp[blockIdx.x * 16 + (threadIdx.x >> 6)][0] += __builtin_amdgcn_s_memtime() - t0;
-#endif
 }
 
 // Producer window: G units (8 samples, 64 B) per producer thread, unit g = ptid + 256 j; only the
@@ -847,10 +815,10 @@ __device__ __forceinline__ void wsProducerTile(const CfFirArgs& a, int Wl, int8_
   wsWait(c, &c->planesFree[set], kCfWaves * (i >> 1));
   int8_t* planes = smem + set * 4 * a.planeStride;
   const float scale = ldexpf(1.0f, sx);
-  const i4v rsrc2 = wsTileRsrc(a, tile + 2, i + 2 < n && !(GSDR_CF_EXPERIMENT & 4));
+  const i4v rsrc2 = wsTileRsrc(a, tile + 2, i + 2 < n);
 #pragma unroll
   for (int j = 0; j < G; ++j) {
-    if (!direct && !(GSDR_CF_EXPERIMENT & 1)) wsSplitGroup<G>(a, Wl, wCur, planes, ptid, scale, j);
+    if (!direct) wsSplitGroup<G>(a, Wl, wCur, planes, ptid, scale, j);
     wsLoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
   }
   if (ptid == 0) c->mode[set] = direct ? kWsDirect : sx;
@@ -874,7 +842,7 @@ __device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* pa
   const int wave = tid >> 6;
   const int b = dbp ? (j & 1) : 0;
   wsWait(c, &c->partsFull[b], kCfWaves * (dbp ? (j >> 1) + 1 : j + 1));
-  if (!(GSDR_CF_EXPERIMENT & 8) && (I8 || mode != kWsDirect)) {
+  if (I8 || mode != kWsDirect) {
     const float* pb = part + b * (kCfPartialBytes / 4);
     float yi = 0.0f, yq = 0.0f;
 #pragma unroll
@@ -980,13 +948,9 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
           if (!I8) n1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
         }
         asm volatile("" ::: "memory");
-        if (GSDR_CF_EXPERIMENT & 2) {
-          acc[s] += (float)x0[0] + (float)x1[1];
-        } else {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
-          if (!I8) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
-        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
+        if (!I8) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
         x0 = n0;
         x1 = n1;
       }
@@ -1036,13 +1000,6 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
   if (n <= 0) return;
 
   const int ptid = tid - kCfThreads;
-#if GSDR_CF_EXPERIMENT & 32
-  const uint64_t tStart = __builtin_amdgcn_s_memtime();
-#define WS_STAMP_END() \
-  if (lane == 0) gWsStamp[blockIdx.x * 16 + wave][1] += __builtin_amdgcn_s_memtime() - tStart
-#else
-#define WS_STAMP_END() (void)0
-#endif
 
   // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), block max; zero both plane sets --------
   if (tid < kWsCtlZeroWords) reinterpret_cast<int*>(c)[tid] = 0;
@@ -1090,14 +1047,11 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
       if (i + 2 >= n) break;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the wave
-    WS_STAMP_END();
     return;
   }
 
   wsConsumers<KS, EPI, false>(a, smem, part, c, sh, t0, n, tid, a.dbp != 0);
-  WS_STAMP_END();
 }
-#undef WS_STAMP_END
 
 // ---- int8 IQ input -------------------------------------------------------------------------
 
@@ -1688,19 +1642,6 @@ hipError_t wsPrepare(int32_t& spinLimit, uint32_t*& abortOut) {
 }
 
 }  // namespace
-
-// Attribution builds (tools/exp/cf_bench): copy out and clear the wave-specialised kernel's stamps.
-hipError_t wsReadStamps(unsigned long long* host) {
-#if GSDR_CF_EXPERIMENT & 32
-  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(gWsStamp), sizeof(gWsStamp));
-  static unsigned long long zeros[256 * 16][2];
-  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(gWsStamp), zeros, sizeof(gWsStamp));
-  return e;
-#else
-  (void)host;
-  return hipErrorNotSupported;
-#endif
-}
 
 bool firCfMfmaEligible(size_t tapCount, size_t decimation, const void* in) {
   const size_t d = decimation < 1 ? 1 : decimation;

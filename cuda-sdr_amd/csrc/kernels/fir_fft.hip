@@ -44,10 +44,6 @@
 #include <atomic>
 #include <cmath>
 
-// Attribution builds only (tools/exp/run_fft_variants.sh); 0 in the product build.
-#ifndef GSDR_FFT_EXP
-#define GSDR_FFT_EXP 0
-#endif
 #ifndef GSDR_FFT_STAGGER
 #define GSDR_FFT_STAGGER 1  // s_sleep(127) rounds before waves 4-7 start (~64 x 127 cycles each)
 #endif
@@ -368,25 +364,10 @@ __device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kCf32
   for (int j = 0; j < 8; ++j) {
 #pragma unroll
     for (int i = 0; i < D / 2; ++i) {
-      const f4 u = (GSDR_FFT_EXP & 2) ? f4{(float)(l + i), (float)j, (float)(b & 7), 1.0f}
-                                      : __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((j * D / 2 + i) * 64 + l) * 16, 0, 0));
+      const f4 u = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((j * D / 2 + i) * 64 + l) * 16, 0, 0));
       R.v[j][2 * i] = f2{u.x, u.y};
       R.v[j][2 * i + 1] = f2{u.z, u.w};
     }
-  }
-  if (GSDR_FFT_EXP & 4) return;
-  if (GSDR_FFT_EXP & 32) {
-    // rows straight from memory: lane l reads row l + 64 j (8 D bytes) as D/2 16-byte loads at a
-    // row stride (the L1 merges the instructions' partial lines); no LDS round trip
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int i = 0; i < D / 2; ++i) {
-        const f4 u = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (l + 64 * j) * D * 8 + i * 16, 0, 0));
-        R.v[j][2 * i] = f2{u.x, u.y};
-        R.v[j][2 * i + 1] = f2{u.z, u.w};
-      }
-    return;
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -546,7 +527,7 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   for (int64_t b = (int64_t)blockIdx.x * kWaves + w; b < a.nBlocks; b += stride) {
     Rows<D, IN> R;
     loadRows<D>(a, b, R, L.scratch, l);
-    if (!(GSDR_FFT_EXP & 8) && blockNeedsDirect<D, IN>(a, R, b, l)) {
+    if (blockNeedsDirect<D, IN>(a, R, b, l)) {
       if (l == 0) atomicAdd(&gDirectBlocks, 1ull);
       directBlock<D, IN, EPI>(a, b, l);
       continue;
@@ -562,7 +543,7 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
       for (int n = 0; n < NP; ++n)
 #pragma unroll
         for (int j = 0; j < 8; ++j) z[n][j] = R.point(j, p + n);
-      if (!(GSDR_FFT_EXP & 1)) fftFwd<NP>(z, L, l);
+      fftFwd<NP>(z, L, l);
 #pragma unroll
       for (int n = 0; n < NP; ++n) {
         f2 g[8], u[8];
@@ -578,13 +559,13 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
         for (int d = 0; d < 8; ++d) acc[0][d] = cmul2(z[n][d], g[d], u[d]);
       }
     }
-    if (!(GSDR_FFT_EXP & 1)) ifft512(acc, L, l);
+    ifft512(acc, L, l);
     const int64_t k0 = b * (int64_t)a.V;
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
       const int m = l + 64 * h;
       const int64_t k = k0 + m;
-      if (m < a.V && k < a.nOut && !((GSDR_FFT_EXP & 16) && a.T > 0)) {
+      if (m < a.V && k < a.nOut) {
         if (EPI == kAm)
           reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc[0][h]);
         else

@@ -58,12 +58,6 @@ constexpr int kI8TileOut = 512;                                        // 16 row
 #ifndef GSDR_I8_BLOCKS_PER_CU
 #define GSDR_I8_BLOCKS_PER_CU 3
 #endif
-#ifndef GSDR_I8_EXPERIMENT
-#define GSDR_I8_EXPERIMENT 0  // attribution builds only: 1 = skip split, 2 = skip MFMA, 4 = skip epilogue,
-                              // 8 = no DMA (compute on stale LDS), 16 = no stores, 32 = clock stamps,
-                              // 64 = hi limb only (half the MFMAs), 128 = one A fragment read per tile,
-                              // 256 = i8 MFMAs in place of the f16 ones (energy probe, wrong results)
-#endif
 constexpr int kI8TilesPerWave = GSDR_I8_TILES_PER_WAVE;
 constexpr int kI8ChunkTiles = kI8Waves * kI8TilesPerWave;              // 8 tiles per chunk
 constexpr int kI8ChunkOut = kI8ChunkTiles * kI8TileOut;                // 4096 outputs per chunk
@@ -209,27 +203,13 @@ __device__ __forceinline__ void tileMfma(const int8_t* planes, const h8 (&bf)[S]
   const int8_t* plane = planes + (row >> 4) * kPlaneBytes;
   const int b0 = tile * 16 + (row & 15);
   acc = v16f{};
-  h8 a0 = h8{};
-  if (GSDR_I8_EXPERIMENT & 128) a0 = *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0, half));
 #pragma unroll
   for (int s = 0; s < S; ++s) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const h8 av = (GSDR_I8_EXPERIMENT & 128) ? a0 + (_Float16)s
-                                               : *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0 + s, 2 * u + half));
-      if constexpr ((GSDR_I8_EXPERIMENT & 256) != 0) {  // energy probe: the same count of i8 MFMAs
-        typedef int v16i __attribute__((ext_vector_type(16)));
-        typedef int v4i __attribute__((ext_vector_type(4)));
-        v16i ia = __builtin_bit_cast(v16i, acc);
-        ia = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(v4i, av), __builtin_bit_cast(v4i, bf[s][u][0]),
-                                                   ia, 0, 0, 0);
-        ia = __builtin_amdgcn_mfma_i32_32x32x32_i8(__builtin_bit_cast(v4i, av), __builtin_bit_cast(v4i, bf[s][u][1]),
-                                                   ia, 0, 0, 0);
-        acc = __builtin_bit_cast(v16f, ia);
-      } else {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][0], acc, 0, 0, 0);
-        if (!(GSDR_I8_EXPERIMENT & 64)) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][1], acc, 0, 0, 0);
-      }
+      const h8 av = *reinterpret_cast<const h8*>(plane + 16 * planeUnit(b0 + s, 2 * u + half));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[s][u][1], acc, 0, 0, 0);
     }
   }
 }
@@ -259,24 +239,8 @@ template <int S, int EPI>
 __device__ __forceinline__ void computeTile(const I8FirArgs& a, const int8_t* planes, const h8 (&bf)[S][2][2],
                                             int64_t chunkOut, int tile, int lane, float outScale) {
   v16f acc;
-  if (GSDR_I8_EXPERIMENT & 2) {
-    acc = v16f{} + (float)*reinterpret_cast<const _Float16*>(planes + 16 * lane);
-  } else {
-    tileMfma<S>(planes, bf, tile, lane, acc);
-  }
+  tileMfma<S>(planes, bf, tile, lane, acc);
   const int64_t tileOut = chunkOut + (int64_t)tile * kI8TileOut;
-  if (GSDR_I8_EXPERIMENT & 16) {  // no stores at all (keeps the accumulator live)
-    if (acc[0] + acc[5] + acc[9] + acc[15] == 1.2345f) reinterpret_cast<float*>(a.out)[lane] = 0.0f;
-    return;
-  }
-  if (GSDR_I8_EXPERIMENT & 4) {
-    const int64_t rowOut = tileOut + 4 * (lane >> 5) * 32 + (lane & 31);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (rowOut + 32 * ((i & 3) + 8 * (i >> 2)) < a.nOut)
-        reinterpret_cast<float*>(a.out)[rowOut + 32 * ((i & 3) + 8 * (i >> 2))] = acc[i];
-    return;
-  }
   if (tileOut + kI8TileOut <= a.nOut) tileEpilogue<EPI, true>(a, acc, tileOut, lane, outScale);
   else tileEpilogue<EPI, false>(a, acc, tileOut, lane, outScale);
 }
@@ -289,7 +253,6 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
   __shared__ __attribute__((aligned(16))) _Float16 limbTab[2 * kLimbRow];
   __shared__ float waveMax[kI8Waves];
 
-  const uint64_t tStart = (GSDR_I8_EXPERIMENT & 32) ? __builtin_amdgcn_s_memrealtime() : 0;
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wave = waveUniform(tid >> 6);
@@ -325,7 +288,7 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
   constexpr int kMaxPerChunk = (G::kPieces + kI8Waves - 1) / kI8Waves;
 #pragma unroll
   for (int j = 0; j < kRing - 1; ++j)
-    if (j < n && !(GSDR_I8_EXPERIMENT & 8))
+    if (j < n)
       issueChunk<S>(alignedBase, lastBlock, T0 + j * kI8ChunkTiles, ringLds + j * G::kSlot, wave, lane);
   reinterpret_cast<uint32_t*>(limbTab)[tid] = 0u;  // 2 rows x 256 f16 = one dword per thread
   vmWaitDyn<0, (kRing - 1) * kMaxPerChunk>(waveUniform(min(kRing - 1, n) * perChunk));
@@ -376,23 +339,16 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
   // from here on the only vector-memory operations are the DMA pieces and the epilogue stores
 
   constexpr int kSteady = (kRing - 2) * kMaxPerChunk + (kRing - 1) * kStoresPerChunk;
-  uint64_t t0c = 0, t0r = 0;
-  if (GSDR_I8_EXPERIMENT & 32) {
-    t0c = __builtin_amdgcn_s_memtime();
-    t0r = __builtin_amdgcn_s_memrealtime();
-  }
-  (void)tStart;
   for (int i = 0; i < n; ++i) {
     // Retire slot i: after its pieces this wave issued min(kRing-2, n-1-i) later chunks' pieces
     // and the stores of min(i, kRing-1) chunks (stores of chunk j follow the pieces of j+kRing-1).
     // (only the last chunk may be partial: its stores follow every wait but the final one)
     const int later = min(kRing - 2, n - 1 - i) * perChunk + min(i, kRing - 1) * kStoresPerChunk;
-    if (GSDR_I8_EXPERIMENT & 8) {
-    } else if (later == kSteady) vmWait<kSteady>();  // the steady state of the widest waves
+    if (later == kSteady) vmWait<kSteady>();  // the steady state of the widest waves
     else vmWaitDyn<0, kSteady>(waveUniform(later));
     ldsBarrier();  // every wave's pieces of slot i landed; compute(i-1) done with the planes
     const int slot = i % kRing;
-    if (!(GSDR_I8_EXPERIMENT & 1)) splitSlot<S>(ring + kRingPad + slot * G::kSlot + sub, planes, sub, tid);
+    splitSlot<S>(ring + kRingPad + slot * G::kSlot + sub, planes, sub, tid);
     if (a.carryDst != nullptr && T0 == 0 && i == 0) {
       // streaming history: the only block that reads samples [0, T - 1) has them in LDS now,
       // so the carry may overwrite them in place (source [nOut, nIn) is disjoint: nOut >= T - 1)
@@ -400,7 +356,7 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
       for (int t = tid; t < T - 1; t += kI8Threads) reinterpret_cast<uint16_t*>(a.carryDst)[t] = src[t];
     }
     // refill the slot chunk i-1 used (its split finished before the barrier above)
-    if (i + kRing - 1 < n && !(GSDR_I8_EXPERIMENT & 8))
+    if (i + kRing - 1 < n)
       issueChunk<S>(alignedBase, lastBlock, T0 + (i + kRing - 1) * kI8ChunkTiles,
                     ringLds + ((i + kRing - 1) % kRing) * G::kSlot, wave, lane);
     ldsBarrier();  // planes complete
@@ -414,16 +370,6 @@ __global__ __launch_bounds__(kI8Threads, GSDR_I8_BLOCKS_PER_CU) void firI8MfmaKe
     }
   }
   vmWait<0>();  // no DMA may still target this block's LDS when it exits
-  if ((GSDR_I8_EXPERIMENT & 32) && tid == 0) {
-    const uint64_t tc = __builtin_amdgcn_s_memtime(), tr = __builtin_amdgcn_s_memrealtime();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    uint32_t* st = reinterpret_cast<uint32_t*>(a.out) + 4 * blockIdx.x;
-    st[0] = (uint32_t)(tc - t0c);
-    st[1] = (uint32_t)(tr - t0r);
-    st[2] = (uint32_t)tStart;
-    st[3] = (uint32_t)t0r;
-    reinterpret_cast<uint32_t*>(a.out)[4 * 768 + blockIdx.x] = (uint32_t)tr;
-  }
 }
 
 namespace {

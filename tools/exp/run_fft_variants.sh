@@ -8,6 +8,8 @@ set -eu
 cd "$(dirname "$0")/../.."
 OUT=tools/exp/_build_fft
 KSRC=cuda-sdr_amd/csrc/kernels/fir_fft.hip
+# the attribution switches live in a patch, applied to a copy (the shipped kernel has none)
+ASRC=${OUT:-tools/exp}/fir_fft_attr.hip
 VARIANTS=${VARIANTS:-"base|
 nofft|-DGSDR_FFT_EXP=1
 noload|-DGSDR_FFT_EXP=2
@@ -21,12 +23,13 @@ rowload_nofft|-DGSDR_FFT_EXP=33
 load_only|-DGSDR_FFT_EXP=29"}
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
+  patch -s -o $ASRC $KSRC tools/exp/attribution/fir_fft.patch
   decls=""; table=""; objs=""; i=0
   while IFS='|' read -r name flags src; do
     [ -z "$name" ] && continue
     hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Iinclude -Icuda-sdr_amd/csrc/kernels \
       -Dgsdr_amd=f$i -DgsdrAmdSetFftGuard=f${i}_sg -DgsdrAmdGetFftGuard=f${i}_gg -DgsdrAmdFftDirectBlocks=f${i}_db \
-      $flags -c ${src:-$KSRC} -o $OUT/f$i.o &
+      $flags -c ${src:-$ASRC} -o $OUT/f$i.o &
     decls="$decls DECL($i)"; table="$table {\"$name\", f$i::launchFirFft},"; objs="$objs $OUT/f$i.o"
     i=$((i+1))
   done <<< "$VARIANTS"

@@ -7,6 +7,8 @@ set -eu
 cd "$(dirname "$0")/../.."
 OUT=tools/exp/_build
 KSRC=cuda-sdr_amd/csrc/kernels/fir_i8_mfma.hip
+# the attribution switches live in a patch, applied to a copy (the shipped kernel has none)
+ASRC=${OUT:-tools/exp}/fir_i8_mfma_attr.hip
 VARIANTS=${VARIANTS:-"base|
 base_clk|-DGSDR_I8_EXPERIMENT=32
 bpc2|-DGSDR_I8_BLOCKS_PER_CU=2
@@ -14,11 +16,12 @@ tiles1|-DGSDR_I8_TILES_PER_WAVE=1
 tiles1_clk|-DGSDR_I8_TILES_PER_WAVE=1 -DGSDR_I8_EXPERIMENT=32"}
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
+  patch -s -o $ASRC $KSRC tools/exp/attribution/fir_i8_mfma.patch
   decls=""; table=""; objs=""; i=0
   while IFS='|' read -r name flags src; do
     [ -z "$name" ] && continue
     hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Iinclude -Icuda-sdr_amd/csrc/kernels -mllvm -amdgpu-mfma-vgpr-form \
-      -Dgsdr_amd=v$i $flags -c ${src:-$KSRC} -o $OUT/v$i.o &
+      -Dgsdr_amd=v$i $flags -c ${src:-$ASRC} -o $OUT/v$i.o &
     decls="$decls DECL($i)"; table="$table {\"$name\", v$i::launchFirI8Mfma},"; objs="$objs $OUT/v$i.o"
     i=$((i+1))
   done <<< "$VARIANTS"
