@@ -530,7 +530,8 @@ __global__ __launch_bounds__(kThreads) void firSmallKernel(FirArgs a) {
 constexpr int kDecR = 4;
 constexpr int kDecThreads = 128;
 constexpr int kDecOut = kDecR * kDecThreads;
-constexpr int kDecLoads = 8;   // float4 staging loads in flight per lane
+constexpr int kDecLoads = 24;  // float4 staging loads in flight per lane: one HBM round trip per
+                               // block at C5's shape (2620 float4 per block), small launches are latency-bound
 constexpr int kDecMaxQ = 32;   // taps per phase
 
 // Per-phase-pair LDS: the window rows (even count: 16 B aligned rows) and the tap pairs (even count)

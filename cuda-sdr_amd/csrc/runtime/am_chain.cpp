@@ -69,8 +69,11 @@ struct gsdrAmChainImpl {
   float* resOut = nullptr;
   size_t resChunks = 0;
   bool resFirst = false;
-  // multi-chunk stepping (gsdrAmChainStepChunks): one cached graph of nChunks chunk steps
+  // multi-chunk stepping (gsdrAmChainStepChunks): one cached graph of nChunks chunk steps over an
+  // AM window [ra history | nChunks La]
   hipGraphExec_t multi = nullptr;
+  float* amMulti = nullptr;
+  size_t amMultiChunks = 0;
   const int8_t* multiIn = nullptr;
   float* multiOut = nullptr;
   size_t multiChunks = 0;
@@ -125,18 +128,35 @@ struct gsdrAmChainImpl {
     return hipSuccess;
   }
 
-  // nChunks consecutive chunk steps from `in` (device, contiguous chunks), audio appended at `out`
+  // nChunks consecutive chunk steps from `in` (device, contiguous chunks), audio appended at `out`.
+  // Each chunk is its own RF and audio launch, as stepping would be; only chunk 0 goes through the
+  // staging window (behind the history carried from the previous step). Chunk i >= 1 reads its RF
+  // history in place - the last r samples of chunk i - 1, right in front of it - and its AM
+  // history in place in amMulti; the carries for the next step are copied out once at the end.
   hipError_t enqueueChunks(const int8_t* in, size_t nChunks, float* out, size_t startStep) {
+    const bool first = startStep == 0;
+    const int p0 = first ? 0 : (int)(startStep & 1);
+    if (!first) {
+      AMC_TRY(hipMemcpyAsync(staging[p0] + 2 * r, in, 2 * L, hipMemcpyDeviceToDevice, stream));
+      AMC_TRY(hipMemcpyAsync(amMulti, am, sizeof(float) * ra, hipMemcpyDeviceToDevice, stream));
+    }
     size_t pos = 0;
     for (size_t i = 0; i < nChunks; ++i) {
-      const size_t step = startStep + i;
-      const int p = step == 0 ? 0 : (int)(step & 1);
-      const size_t n = step == 0 ? na1 : naSteady;
-      AMC_TRY(hipMemcpyAsync(staging[p] + 2 * r, in + 2 * L * i, 2 * L, hipMemcpyDeviceToDevice, stream));
-      AMC_TRY(enqueueCompute(step == 0, p));
-      AMC_TRY(hipMemcpyAsync(out + pos, audio, sizeof(float) * n, hipMemcpyDeviceToDevice, stream));
-      pos += n;
+      const bool f = first && i == 0;
+      const size_t nRf = f ? n1 : La;
+      const int8_t* rfIn = f ? in : (i == 0 ? staging[p0] : in + 2 * (L * i - r));
+      const size_t amEnd = ra + (i + 1) * La;  // chunk i's AM ends here (first step: n1 < La of it)
+      AMC_TRY(gsdrInt8FirFCAmDemod(D, taps, T, rfIn, amMulti + amEnd - nRf, nRf, device, stream));
+      // one stream: forking chunk i's audio FIR onto a second captured stream beside chunk i+1's
+      // RF launch measured 3.5x slower per chunk (cross-stream graph dependencies)
+      const size_t na = f ? na1 : naSteady;
+      AMC_TRY(gsdrFirFF(Da, audioTaps, Ta, amMulti + (f ? amEnd - n1 : amEnd - La - ra), out + pos, na, device,
+                        stream));
+      pos += na;
     }
+    const int pn = (int)((startStep + nChunks) & 1);
+    AMC_TRY(hipMemcpyAsync(staging[pn], in + 2 * (L * nChunks - r), 2 * r, hipMemcpyDeviceToDevice, stream));
+    AMC_TRY(hipMemcpyAsync(am, amMulti + nChunks * La, sizeof(float) * ra, hipMemcpyDeviceToDevice, stream));
     return hipSuccess;
   }
 
@@ -160,6 +180,7 @@ struct gsdrAmChainImpl {
     (void)hipFree(amBig);
     if (resident) (void)hipGraphExecDestroy(resident);
     if (multi) (void)hipGraphExecDestroy(multi);
+    (void)hipFree(amMulti);
     (void)hipFree(audio);
     if (hostIn) (void)hipHostFree(hostIn);
     if (hostOut) (void)hipHostFree(hostOut);
@@ -291,6 +312,16 @@ hipError_t gsdrAmChainStepChunks(gsdrAmChain c, const int8_t* inputIq, size_t nC
   AMC_TRY(push.err);
   const size_t n = gsdrAmChainChunksOutputCount(c, nChunks);
   const int key = c->steps == 0 ? 2 : (int)(c->steps & 1);
+  if (nChunks > c->amMultiChunks) {  // grow the AM window (outside any capture)
+    AMC_TRY(hipStreamSynchronize(c->stream));
+    if (c->multi != nullptr) (void)hipGraphExecDestroy(c->multi);
+    c->multi = nullptr;
+    (void)hipFree(c->amMulti);
+    c->amMulti = nullptr;
+    c->amMultiChunks = 0;
+    AMC_TRY(hipMalloc(&c->amMulti, sizeof(float) * (c->ra + nChunks * c->La)));
+    c->amMultiChunks = nChunks;
+  }
   if (c->multi == nullptr || c->multiIn != inputIq || c->multiOut != output || c->multiChunks != nChunks ||
       c->multiKey != key) {
     if (c->multi != nullptr) {

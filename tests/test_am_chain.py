@@ -140,8 +140,9 @@ def test_am_chain_multi_chunk_graph_matches_steps(chain_mod, orc):
     rf = orc.lowpass_taps(T, 0.04)
     au = orc.lowpass_taps(Ta, 0.02)
     plan = [3, 2, 3, 3]  # parities 0/1 at the start of each batch, the cached graph reused
+    tail = 2  # then single steps: the batches leave the carries where per-chunk stepping reads them
     total = sum(plan)
-    iq = rng.integers(-128, 128, size=2 * L * total).astype(np.int8)
+    iq = rng.integers(-128, 128, size=2 * L * (total + tail)).astype(np.int8)
     dev = torch.from_numpy(iq).cuda()
     multi = chain_mod.AmChain(rf, D, au, Da, L)
     got, pos = [], 0
@@ -150,9 +151,11 @@ def test_am_chain_multi_chunk_graph_matches_steps(chain_mod, orc):
         cnt = multi.step_chunks(dev[2 * L * pos:], n, out)
         got.append(out[:cnt].cpu().numpy())
         pos += n
+    for s in range(total, total + tail):
+        got.append(multi.step(dev[2 * L * s: 2 * L * (s + 1)]).cpu().numpy())
     got = np.concatenate(got)
     per = chain_mod.AmChain(rf, D, au, Da, L)
-    ref = np.concatenate([per.step(dev[2 * L * s: 2 * L * (s + 1)]).cpu().numpy() for s in range(total)])
+    ref = np.concatenate([per.step(dev[2 * L * s: 2 * L * (s + 1)]).cpu().numpy() for s in range(total + tail)])
     assert got.tobytes() == ref.tobytes()
     want, bound = _expected(orc, iq, rf, D, au, Da)
     assert np.all(np.abs(got - want) <= bound)
