@@ -1,31 +1,32 @@
 #!/usr/bin/env python3
 """Benchmark: Msamples/s through the FIR -> QuadAmDemod chain on MI355X (BASELINE.json metric).
 
-Default workload (N=1 and every N, weak scaling): BASELINE.json configs[1] ("C2"):
-HackRF-shaped int8 IQ at 20 Msps -> cf32 convert -> 127-tap complex FIR -> QuadAmDemod.
-One step = one second of signal per GPU (20 M IQ samples), inputs resident in HBM.
-The whole chain runs as the fused gfx950 kernel gsdrInt8FirFCAmDemod (== the chain
-gsdrInt8ToNormFloat -> gsdrFirFC -> gsdrQuadAmDemod, bit for bit; tests/test_gpu_parity.py).
+Default workload (--workload c3, the north-star config): 2^28 - 6 cf32 samples per GPU step ->
+1023-tap real-tap (FC) FIR, D = 10 -> QuadAmDemod, inputs resident in HBM. The FIR+AM runs as
+gsdrFirFCAmDemod, which takes the polyphase overlap-save FFT kernel (fir_fft.hip) at this shape.
+One GPU: the step is ONE launch over [T-1 history | segment]; the input / output buffer sets
+rotate so that a step's working set is never resident in the 256 MiB Infinity Cache.
 
-One GPU: the step is ONE launch over the buffer [T-1 history | segment] that also writes the
-history for the next step (gsdrInt8FirFCAmDemodCarry; for T <= 129, D = 1 the exact f16 MFMA
-kernel firI8MfmaKernel).
+Multi-GPU (one process per GPU, torch.distributed over RCCL; `--gpus N` without a launcher
+spawns the N ranks itself): the stream is time-sharded (gpusdr/shard.py). In step s rank g owns
+samples [(s G + g) L, (s G + g + 1) L) and needs the preceding T - 1 samples, which live on rank
+g - 1 (rank 0: rank G - 1's segment of the previous step): one ring exchange per step, overlapped
+with the bulk launch that needs no halo; a head launch finishes the outputs that read the halo.
+`--backend gloo --share-gpu` runs the same protocol with the ranks on one GPU (halos staged
+through host memory), for testing.
 
-Multi-GPU (one process per GPU, torch.distributed over RCCL): the stream is time-sharded.
-In step s rank g owns stream samples [(s*G + g)*L, (s*G + g + 1)*L) and needs the
-preceding T-1 samples as a halo, which live on rank g-1 (rank 0: rank G-1's segment of the
-previous step). Each step therefore does one ring exchange (isend tail -> g+1, irecv
-halo <- g-1, RCCL over xGMI), overlapped with the bulk kernel that needs no halo; a small
-head kernel finishes the first T-1 outputs once the halo has landed.
-
-Other workloads (--workload): c3 (cf32 2^28, 1023 taps, D=10, FIR->AM), c4 (cf32, 1023 taps,
-D=1, FIR->AM), c5 (the full AM receive chain int8 IQ -> 1023-tap FIR, D=10 -> AM -> 255-tap audio
-FIR, D=20 through the gsdrAmChain executor: one hipGraph launch per 5 M-sample chunk, 1 s of a
-1 Gsps stream split over 8 GPUs = 125 M samples per GPU step; ranks own disjoint time ranges and
-are primed by the warm-up steps, so no data-path collective).
+Other workloads: c2 (BASELINE configs[1]: HackRF int8 IQ at 20 Msps, 127 taps, D = 1, the fused
+gsdrInt8FirFCAmDemodCarry on the int8 MFMA kernel), c4 (cf32, 1023 taps, D = 1), c5 (the full AM
+receive chain int8 IQ -> 1023-tap FIR, D = 10 -> AM -> 255-tap audio FIR, D = 20, 125 M samples
+per GPU step; default `--c5-mode sharded`: time-sharded with the cascaded halo (Ta-1) D + T-1,
+rounded to 3 600 samples; `resident` / `chunked`: the gsdrAmChain executor over one resident
+segment, as one graph / as 25 chunk steps of 5 M samples in one cached graph).
 
 Output: one JSON line on rank 0 (contract in the task statement) with `roofline` for the
-dominant kernel (HIP events on its stream) and `cpu_baseline` (oracle port, rank 0, N=1).
+dominant kernel (HIP events on its stream; `traffic` from the committed rocprofv3 PMC summary
+profiles/pmc_traffic.json), `arithmetic` naming the kernel's number format, and `cpu_baseline`
+(the oracle's float32 direct form on the host's cores, rank 0, N = 1, with the C1 config as a
+second CPU line).
 """
 from __future__ import annotations
 
