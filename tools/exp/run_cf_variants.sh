@@ -16,7 +16,7 @@ mfma_only|-DGSDR_CF_EXPERIMENT=29
 no_mfma_no_split|-DGSDR_CF_EXPERIMENT=3"}
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
-  patch -s -o $ASRC $KSRC tools/exp/attribution/fir_cf_mfma.patch
+  patch -s -o $ASRC $KSRC tools/exp/attribution/fir_cf_mfma.patch || echo "attribution patch does not apply to the current kernel (variants naming a source still build)"
   decls=""; table=""; objs=""; i=0
   while IFS='|' read -r name flags; do
     [ -z "$name" ] && continue

@@ -23,7 +23,7 @@ rowload_nofft|-DGSDR_FFT_EXP=33
 load_only|-DGSDR_FFT_EXP=29"}
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
-  patch -s -o $ASRC $KSRC tools/exp/attribution/fir_fft.patch
+  patch -s -o $ASRC $KSRC tools/exp/attribution/fir_fft.patch || echo "attribution patch does not apply to the current kernel (variants naming a source still build)"
   decls=""; table=""; objs=""; i=0
   while IFS='|' read -r name flags src; do
     [ -z "$name" ] && continue

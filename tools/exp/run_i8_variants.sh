@@ -16,7 +16,7 @@ tiles1|-DGSDR_I8_TILES_PER_WAVE=1
 tiles1_clk|-DGSDR_I8_TILES_PER_WAVE=1 -DGSDR_I8_EXPERIMENT=32"}
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
-  patch -s -o $ASRC $KSRC tools/exp/attribution/fir_i8_mfma.patch
+  patch -s -o $ASRC $KSRC tools/exp/attribution/fir_i8_mfma.patch || echo "attribution patch does not apply to the current kernel (variants naming a source still build)"
   decls=""; table=""; objs=""; i=0
   while IFS='|' read -r name flags src; do
     [ -z "$name" ] && continue
