@@ -263,7 +263,9 @@ uint32_t gspDriverDoFilterGraphed(gspHandle driver, gspHandle queue) {
 }
 
 uint32_t gspDriverGraphStats(gspHandle driver, size_t* eager, size_t* captured, size_t* replayed) {
-  auto* d = dynamic_cast<gsdr_rt::SteppingDriver*>(as<IDriver>(driver));
+  IDriver* any = as<IDriver>(driver);
+  auto* d = dynamic_cast<gsdr_rt::SteppingDriver*>(any);
+  if (d == nullptr) d = gsdr_rt::componentSteppingDriver(any);  // a JSON Component's inner driver
   if (d == nullptr) return Status_InvalidArgument;
   const auto st = d->graphStats();
   if (eager) *eager = st.eager;

@@ -9,6 +9,7 @@
 #include <string>
 #include <unordered_map>
 
+#include "driver.h"
 #include "json.h"
 
 namespace gsdr_rt {
@@ -209,10 +210,15 @@ class PortRemappingSourceFactory final : public IPortRemappingSourceFactory {
 // ---- FilterDriver (FilterDriver.cpp) ------------------------------------------------------------------
 // A Filter whose input is an inner node's sink (setDriverInput) and whose output is an inner node's
 // source (setDriverOutput); committing input steps the inner graph once, and reading output steps it
-// when the output node has nothing yet.
+// when the output node has nothing yet. MI355X extension: with a graph stream set (JSON
+// "hipGraphCommandQueue"), each inner step runs through SteppingDriver::doFilterGraphed, so a
+// component in steady state replays its whole step as one cached hipGraph.
 class FilterDriver final : public IFilterDriver {
  public:
   explicit FilterDriver(ISteppingDriver* stepping) noexcept : mStepping(stepping) {}
+
+  void setGraphStream(hipStream_t stream) noexcept { mGraphStream = stream; }
+  SteppingDriver* stepping() const noexcept { return dynamic_cast<SteppingDriver*>(mStepping.get()); }
 
   void setDriverInput(Sink* sink) noexcept final { mInput = sink; }
   void setDriverOutput(Source* source) noexcept final { mOutput = source; }
@@ -279,7 +285,7 @@ class FilterDriver final : public IFilterDriver {
       return Status_InvalidState;
     }
     FWD_IF_ERR(in->commitBuffer(port, byteCount));
-    return mStepping->doFilter();
+    return step();
   }
   // The reference dereferences a null delegate here (FilterDriver.cpp:290-294); 0 / null, logged.
   size_t preferredInputBufferSize(size_t port) noexcept final {
@@ -298,7 +304,7 @@ class FilterDriver final : public IFilterDriver {
       gslogw("Cannot use FilterDriver as a Source until a node is set via setDriverOutput()");
       return 0;
     }
-    if (out->getOutputDataSize(port) == 0 && mStepping->doFilter() != Status_Success) return 0;
+    if (out->getOutputDataSize(port) == 0 && step() != Status_Success) return 0;
     return out->getOutputDataSize(port);
   }
   size_t getOutputSizeAlignment(size_t port) noexcept final {
@@ -321,11 +327,17 @@ class FilterDriver final : public IFilterDriver {
     }
     bool all = true;
     for (size_t p = 0; p < numPorts; ++p) all = all && out->getOutputDataSize(p) != 0;
-    if (!all) FWD_IF_ERR(mStepping->doFilter());
+    if (!all) FWD_IF_ERR(step());
     return out->readOutput(portOutputBuffers, numPorts);
   }
 
  private:
+  Status step() noexcept {
+    if (mGraphStream != nullptr) {
+      if (SteppingDriver* d = stepping()) return d->doFilterGraphed(mGraphStream);
+    }
+    return mStepping->doFilter();
+  }
   struct Callback {
     FilterDriver* self;
     void* context;
@@ -336,6 +348,7 @@ class FilterDriver final : public IFilterDriver {
   ConstRef<ISteppingDriver> mStepping;
   Ref<Sink> mInput;
   Ref<Source> mOutput;
+  hipStream_t mGraphStream = nullptr;
   REF_COUNTED(FilterDriver);
 };
 
@@ -474,6 +487,16 @@ class FilterDriverFactory final : public IFilterDriverFactory {
         FWD_IN_RESULT_IF_ERR(mapOutput(out->string(), 0, 0));
       }
       if (outMapper != nullptr) component->setDriverOutput(outMapper.get().get());
+      // MI355X extension: replay the inner graph's steady-state steps as hipGraphs on this queue
+      if (const Json* gq = params.get("hipGraphCommandQueue"); gq != nullptr) {
+        if (!gq->isString()) {
+          gsloge("\"hipGraphCommandQueue\" must name a command queue");
+          return ERR_RESULT(Status_ParseError);
+        }
+        Ref<ICudaCommandQueue> queue;
+        UNWRAP_OR_FWD_RESULT(queue, mF->getCommandQueueFactory()->getCudaCommandQueue(gq->string().c_str()));
+        static_cast<FilterDriver*>(component)->setGraphStream(queue->cudaStream());
+      }
 
       if (const Json* conns = params.get("connections"); conns != nullptr && conns->isArray()) {
         for (const Json& c : conns->array()) {
@@ -700,6 +723,10 @@ class ReadByteCountMonitorFactory final : public IReadByteCountMonitorFactory {
 }  // namespace
 
 IFilterDriverFactory* newFilterDriverFactory(IFactories* f) noexcept { return new (std::nothrow) FilterDriverFactory(f); }
+SteppingDriver* componentSteppingDriver(IDriver* driver) noexcept {
+  auto* fd = dynamic_cast<FilterDriver*>(driver);
+  return fd == nullptr ? nullptr : fd->stepping();
+}
 IPortRemappingSinkFactory* newPortRemappingSinkFactory() noexcept { return new (std::nothrow) PortRemappingSinkFactory(); }
 IPortRemappingSourceFactory* newPortRemappingSourceFactory() noexcept {
   return new (std::nothrow) PortRemappingSourceFactory();

@@ -24,6 +24,10 @@ Status designLowPass(double sampleRate, double cutoff, double transitionWidth, d
                      std::vector<float>& taps) noexcept;
 
 IFilterDriverFactory* newFilterDriverFactory(IFactories* factories) noexcept;
+
+class SteppingDriver;
+// The stepping driver inside a component (FilterDriver), or nullptr if `driver` is not one.
+SteppingDriver* componentSteppingDriver(IDriver* driver) noexcept;
 IPortRemappingSinkFactory* newPortRemappingSinkFactory() noexcept;
 IPortRemappingSourceFactory* newPortRemappingSourceFactory() noexcept;
 IRfToPcmAudioFactory* newRfToPcmAudioFactory(IFactories* factories) noexcept;

@@ -189,6 +189,12 @@ class Node(_Handle):
         super().__init__(ptr)
         self.queue = queue
 
+    def graph_stats(self):
+        """A JSON Component's inner stepping: plain, capturing and replayed steps (hipGraph)."""
+        e, c, r = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        _check(_L().gspDriverGraphStats(self._h, ctypes.byref(e), ctypes.byref(c), ctypes.byref(r)), "graphStats")
+        return {"eager": e.value, "captured": c.value, "replayed": r.value}
+
     # -- constructors mirroring the reference factories --
     @classmethod
     def fir(cls, queue: Queue, taps: np.ndarray, decimation: int = 1, element_type: int = SAMPLE_FLOAT_COMPLEX):

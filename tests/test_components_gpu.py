@@ -92,6 +92,38 @@ def test_json_component_of_gpu_fir_and_am(graph, q0, orc):
     assert np.all(np.abs(got - np.abs(y64)) <= FIR_TOL * bound + 1e-30)
 
 
+def test_json_component_replays_steps_as_hip_graphs(graph, q0, orc):
+    """"hipGraphCommandQueue": the component's inner steps go through doFilterGraphed - the
+    steady-state steps replay cached hipGraphs, bit-equal to the eagerly stepped component."""
+    T, D = 127, 4
+    taps = orc.lowpass_taps(T, 0.1)
+    body = ('"nodes": {"lpf": {"type": "Fir", "commandQueue": "q0", "tapType": "Float", '
+            '"elementType": "FloatComplex", "decimation": %d, "taps": [%s]}, '
+            '"am": {"type": "QuadDemod", "modulation": "am", "sampleRate": 1e6, "commandQueue": "q0"}}, '
+            '"connections": [{"source": "lpf", "sink": "am"}], '
+            '"inputPorts": [{"exposedPort": 0, "mapped": {"node": "lpf", "port": 0}}], '
+            '"outputPort": "am"') % (D, ",".join("%.9g" % t for t in taps))
+    eager = graph.Node.from_json("Component", "{%s}" % body, q0)
+    graphed = graph.Node.from_json("Component", '{%s, "hipGraphCommandQueue": "q0"}' % body, q0)
+    rng = np.random.default_rng(5)
+    chunk = 8_192  # equal pushes: a repeating window state after the first steps
+    x = (rng.standard_normal(chunk * 24) + 1j * rng.standard_normal(chunk * 24)).astype(np.complex64)
+    outs = {}
+    for name, comp in (("eager", eager), ("graphed", graphed)):
+        got = []
+        for a in range(0, len(x), chunk):
+            comp.push(x[a:a + chunk])
+            got.append(_read_all(graph, q0, comp, 4, np.float32, cap_elems=1 << 14))
+        outs[name] = np.concatenate(got)
+    assert outs["graphed"].tobytes() == outs["eager"].tobytes()
+    st = graphed.graph_stats()
+    assert st["replayed"] > 0, st
+    assert eager.graph_stats()["replayed"] == 0
+    y64, bound = orc.fir_f64(taps, x, D)
+    assert len(outs["graphed"]) == len(y64)
+    assert np.all(np.abs(outs["graphed"] - np.abs(y64)) <= FIR_TOL * bound + 1e-30)
+
+
 def test_rf_to_pcm_audio_component(graph, q0, orc):
     f32 = np.float32
     rf_rate, rf_dec, au_dec = 1e6, 5, 4
