@@ -9,6 +9,7 @@
 
 #include "../runtime/composite.h"
 #include "../runtime/driver.h"
+#include "../runtime/filters.h"
 
 namespace {
 
@@ -182,6 +183,33 @@ uint32_t gspHostBufferCreate(gspHandle queue, size_t bytes, gspHandle* bufferOut
   UNWRAP_OR_FWD_STATUS(alloc, factories()->getCudaAllocatorFactory()->createCudaAllocator(q, 32, true));
   UNWRAP_OR_FWD_STATUS(bf, factories()->createBufferFactory(alloc.get().get()));
   return give(bf.get()->createBuffer(bytes), bufferOut);
+}
+
+uint32_t gspHostSinkCreate(gspHandle queue, gspHandle* sinkOut) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (q == nullptr) return Status_InvalidArgument;
+  return give(gsdr_rt::HostEgressSink::create(q, factories()), sinkOut);
+}
+
+uint32_t gspHostSinkAvailable(gspHandle sink, size_t* bytesOut) {
+  auto* s = as<gsdr_rt::HostEgressSink>(sink);
+  if (s == nullptr || bytesOut == nullptr) return Status_InvalidArgument;
+  *bytesOut = s->available();
+  return Status_Success;
+}
+
+uint32_t gspHostSinkRead(gspHandle sink, void* dst, size_t capacity, size_t* bytesOut) {
+  auto* s = as<gsdr_rt::HostEgressSink>(sink);
+  if (s == nullptr || (dst == nullptr && capacity != 0)) return Status_InvalidArgument;
+  const size_t n = s->read(dst, capacity);
+  if (bytesOut) *bytesOut = n;
+  return Status_Success;
+}
+
+uint32_t gspHostSinkFlush(gspHandle sink) {
+  auto* s = as<gsdr_rt::HostEgressSink>(sink);
+  if (s == nullptr) return Status_InvalidArgument;
+  return s->flush();
 }
 
 uint32_t gspDesignLowPass(double sampleRate, double cutoff, double transitionWidth, double dbAttenuation, float* taps,

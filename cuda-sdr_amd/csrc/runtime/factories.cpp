@@ -240,6 +240,26 @@ class MemcpyFilterFactory final : public ICudaMemcpyFilterFactory {
   REF_COUNTED(MemcpyFilterFactory);
 };
 
+// ---- host egress sink (MI355X extension: the AAC writer's D2H + wait-previous path without the codec) ----
+class HostSinkFactory final : public INodeFactory {
+ public:
+  explicit HostSinkFactory(IFactories* f) noexcept : mF(f) {}
+  Result<Node> create(const char* jsonParameters) noexcept final {
+    try {
+      Json p;
+      if (!parseParams(jsonParameters, p)) return ERR_RESULT(Status_ParseError);
+      Ref<ICudaCommandQueue> q;
+      UNWRAP_OR_FWD_RESULT(q, queueFromParams(mF, p));
+      return ResultCast<Node>(HostEgressSink::create(q.get().get(), mF));
+    }
+    IF_CATCH_RETURN_RESULT;
+  }
+
+ private:
+  IFactories* const mF;
+  REF_COUNTED(HostSinkFactory);
+};
+
 // ---- out-of-scope factories: valid objects whose creators report Status_NotFound ----------------------------
 #define GS_OUT_OF_SCOPE(what__)            \
   do {                                     \
@@ -556,6 +576,12 @@ GS_EXPORT Status registerDefaultNodeFactories() noexcept {
   FWD_IF_ERR(registerNodeFactory("MultiplyCCC", F->getMultiplyFactory()));
   FWD_IF_ERR(registerNodeFactory("QuadDemod", F->getQuadDemodFactory()));
   FWD_IF_ERR(registerNodeFactory("HipMemcpy", F->getCudaMemcpyFilterFactory()));
+  // extension: the host egress sink (D2H end of a chain, one step in flight)
+  {
+    Ref<INodeFactory> hostSink(new (std::nothrow) HostSinkFactory(F));
+    if (hostSink == nullptr) return Status_OutOfMemory;
+    FWD_IF_ERR(registerNodeFactory("HostSink", hostSink.get().get()));
+  }
   // extension: the RF -> PCM component by name (the reference only reaches it through IFactories)
   FWD_IF_ERR(registerNodeFactory("RfToPcmAudio", F->getRfToPcmAudioFactory()));
   return Status_Success;

@@ -1,5 +1,7 @@
 #include "filters.h"
 
+#include <cstring>
+
 #include <gsdr/conversion.h>
 #include <gsdr/gsdr.h>
 #include <gsdr/gsdr_amd.h>
@@ -458,6 +460,74 @@ Status HipMemcpyFilter::readOutput(IBuffer** portOutputBuffers, size_t portCount
   FWD_IF_ERR(mCopier->copy(out->writePtr(), in->readPtr(), n));
   FWD_IF_ERR(out->range()->increaseEndOffset(n));
   return consumeInputBytesAndMoveUsedToStart(0, n);
+}
+
+// ---- host egress (AacFileWriter.cpp:267-280 minus the codec; Waiter.cpp:34-50) ---------------------------
+Result<Sink> HostEgressSink::create(ICudaCommandQueue* queue, IFactories* factories) noexcept {
+  NON_NULL_PARAM_OR_RET(queue);
+  Ref<IRelocatableResizableBufferFactory> windows;
+  UNWRAP_OR_FWD_RESULT(windows, factories->createRelocatableCudaBufferFactory(queue, 32, true));  // pinned host
+  return makeRefResultNonNull<Sink>(
+      new (std::nothrow) HostEgressSink(windows.get().get(), factories->getBufferSliceFactory(), queue));
+}
+
+HostEgressSink::HostEgressSink(IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
+                               ICudaCommandQueue* queue) noexcept
+    : BaseSink(windows, slices, 1), mQueue(queue), mWaiter(queue->cudaDevice(), queue->cudaStream()) {}
+
+Result<IBuffer> HostEgressSink::requestBuffer(size_t port, size_t byteCount) noexcept {
+  // the window would be compacted or grown by a stream-ordered copy: let the in-flight step land
+  // and hand it over first, so no byte is read on the host while a copy may still move it
+  bool fits = true;
+  if (mInFlight != 0) {
+    Ref<IBuffer> in;
+    UNWRAP_OR_FWD_RESULT(in, getPortInputBuffer(port));
+    fits = in->range()->remaining() >= byteCount;
+  }
+  if (!fits) {
+    FWD_IN_RESULT_IF_ERR(mWaiter.waitAll());
+    FWD_IN_RESULT_IF_ERR(deliver(0));
+  }
+  return BaseSink::requestBuffer(port, byteCount);
+}
+
+Status HostEgressSink::commitBuffer(size_t port, size_t byteCount) noexcept {
+  FWD_IF_ERR(BaseSink::commitBuffer(port, byteCount));
+  FWD_IF_ERR(mWaiter.recordNextAndWaitPrevious());  // everything before this commit is complete
+  mInFlight = byteCount;
+  return deliver(byteCount);
+}
+
+Status HostEgressSink::deliver(size_t keepInFlight) noexcept {
+  Ref<IBuffer> in;
+  UNWRAP_OR_FWD_STATUS(in, getPortInputBuffer(0));
+  const size_t used = in->range()->used();
+  const size_t ready = used > keepInFlight ? used - keepInFlight : 0;
+  if (ready == 0) return Status_Success;
+  try {
+    if (mReadPos != 0 && mReadPos == mFifo.size()) {
+      mFifo.clear();
+      mReadPos = 0;
+    }
+    const uint8_t* src = in->readPtr();
+    mFifo.insert(mFifo.end(), src, src + ready);
+  } catch (...) {
+    return Status_OutOfMemory;
+  }
+  if (keepInFlight == 0) mInFlight = 0;
+  return consumeInputBytesAndMoveUsedToStart(0, ready);
+}
+
+size_t HostEgressSink::read(void* dst, size_t capacity) noexcept {
+  const size_t n = std::min(capacity, available());
+  if (n != 0) memcpy(dst, mFifo.data() + mReadPos, n);
+  mReadPos += n;
+  return n;
+}
+
+Status HostEgressSink::flush() noexcept {
+  FWD_IF_ERR(mWaiter.waitAll());
+  return deliver(0);
 }
 
 }  // namespace gsdr_rt

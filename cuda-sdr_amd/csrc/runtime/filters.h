@@ -5,6 +5,8 @@
 // queue's stream and returns without synchronising, as in the reference.
 #pragma once
 
+#include "waiter.h"
+
 #include <gpusdrpipeline/Factories.h>
 #include <gpusdrpipeline/abi/base_filters.h>
 #include <gpusdrpipeline/abi/errors.h>
@@ -187,6 +189,35 @@ class HipMemcpyFilter final : public BaseFilter, public IGraphStepState {
   ConstRef<IBufferCopier> mCopier;
   ConstRef<ICudaCommandQueue> mQueue;
   REF_COUNTED(HipMemcpyFilter);
+};
+
+// Egress: the host end of a chain (reference AacFileWriter.cpp:267-280 minus the codec, with the
+// Waiter of Waiter.cpp:34-50). The input window is pinned host memory, so the upstream kernel
+// writes its output straight into it. commitBuffer records an event after the committed work and
+// waits for the PREVIOUS commit's event: one step stays in flight (the stream stays full) while
+// every byte committed before it is moved to the host FIFO that read() drains. flush() waits for
+// the in-flight step and delivers it too.
+class HostEgressSink final : public BaseSink {
+ public:
+  static Result<Sink> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
+  Result<IBuffer> requestBuffer(size_t port, size_t byteCount) noexcept final;
+  Status commitBuffer(size_t port, size_t byteCount) noexcept final;
+  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+
+  size_t available() const noexcept { return mFifo.size() - mReadPos; }
+  size_t read(void* dst, size_t capacity) noexcept;
+  Status flush() noexcept;
+
+ private:
+  HostEgressSink(IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
+                 ICudaCommandQueue* queue) noexcept;
+  Status deliver(size_t keepInFlight) noexcept;
+  ConstRef<ICudaCommandQueue> mQueue;
+  Waiter mWaiter;
+  size_t mInFlight = 0;  // bytes of the last commit, possibly still being written
+  std::vector<uint8_t> mFifo;
+  size_t mReadPos = 0;
+  REF_COUNTED(HostEgressSink);
 };
 
 }  // namespace gsdr_rt

@@ -53,6 +53,10 @@ def _L():
             "gspSourceRead": ([h, ph, sz], u32),
             "gspBufferCreate": ([h, sz, ph], u32),
             "gspHostBufferCreate": ([h, sz, ph], u32),
+            "gspHostSinkCreate": ([h, ph], u32),
+            "gspHostSinkAvailable": ([h, psz], u32),
+            "gspHostSinkRead": ([h, vp, sz, psz], u32),
+            "gspHostSinkFlush": ([h], u32),
             "gspDesignLowPass": ([ctypes.c_double] * 4 + [vp, sz, psz], u32),
             "gspBufferSlice": ([h, sz, sz, ph], u32),
             "gspBufferRange": ([h, psz, psz, psz], u32),
@@ -207,6 +211,28 @@ class Node(_Handle):
     @classmethod
     def quad_am_demod(cls, queue: Queue):
         return cls(_create(_L().gspQuadAmDemodCreate, queue.handle, what="gspQuadAmDemodCreate"), queue)
+
+    @classmethod
+    def host_sink(cls, queue: Queue):
+        """The host egress sink (gspHostSinkCreate): one step in flight, the rest in a host FIFO."""
+        return cls(_create(_L().gspHostSinkCreate, queue.handle, what="gspHostSinkCreate"), queue)
+
+    def host_available(self):
+        n = ctypes.c_size_t()
+        _check(_L().gspHostSinkAvailable(self._h, ctypes.byref(n)), "hostSinkAvailable")
+        return n.value
+
+    def host_read(self, dtype, max_bytes=None):
+        """Drain the host sink's FIFO as an array of `dtype`."""
+        cap = self.host_available() if max_bytes is None else max_bytes
+        out = np.empty(cap, dtype=np.uint8)
+        n = ctypes.c_size_t()
+        _check(_L().gspHostSinkRead(self._h, out.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(n)),
+               "hostSinkRead")
+        return out[:n.value].view(dtype)
+
+    def host_flush(self):
+        _check(_L().gspHostSinkFlush(self._h), "hostSinkFlush")
 
     @classmethod
     def int8_to_float(cls, queue: Queue):

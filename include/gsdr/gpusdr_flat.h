@@ -70,6 +70,15 @@ GSP_API uint32_t gspBufferCreate(gspHandle queue, size_t bytes, gspHandle* buffe
 /* Pinned host buffers (hipHostMalloc through the queue's allocator): outputs of the D2H staging
  * filter. gspBufferBase is then a host pointer. */
 GSP_API uint32_t gspHostBufferCreate(gspHandle queue, size_t bytes, gspHandle* bufferOut);
+/* Host egress sink (JSON type "HostSink"; the D2H end of a chain, reference AacFileWriter.cpp:267-280
+ * without the codec, Waiter.cpp:34-50): its input window is pinned host memory the upstream kernel
+ * writes into; each commit leaves one step in flight and hands everything before it to a host FIFO.
+ * gspHostSinkRead drains up to `capacity` bytes (count in *bytesOut); gspHostSinkFlush waits for the
+ * in-flight step and queues it too. */
+GSP_API uint32_t gspHostSinkCreate(gspHandle queue, gspHandle* sinkOut);
+GSP_API uint32_t gspHostSinkAvailable(gspHandle sink, size_t* bytesOut);
+GSP_API uint32_t gspHostSinkRead(gspHandle sink, void* dst, size_t capacity, size_t* bytesOut);
+GSP_API uint32_t gspHostSinkFlush(gspHandle sink);
 GSP_API uint32_t gspBufferSlice(gspHandle buffer, size_t start, size_t end, gspHandle* sliceOut);
 GSP_API uint32_t gspBufferRange(gspHandle buffer, size_t* offset, size_t* endOffset, size_t* capacity);
 GSP_API uint32_t gspBufferSetRange(gspHandle buffer, size_t offset, size_t endOffset);

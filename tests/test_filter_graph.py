@@ -349,3 +349,46 @@ def test_graph_stepping_falls_back_for_a_tone_source(graph, orc):
             assert st["captured"] == 0 and st["replayed"] == 0 and st["eager"] == 6, st
     assert outs["graphed"].tobytes() == outs["eager"].tobytes()
     assert len(outs["eager"]) > 0
+
+
+def test_host_egress_sink_keeps_one_step_in_flight(graph, orc):
+    """The host egress sink (reference AacFileWriter.cpp:267-280 without the codec, Waiter.cpp:34-50)
+    at the tail of int8 -> cf32 -> FIR -> AM: the AM kernel writes into the sink's pinned host
+    window; after each step everything but that step's bytes is in the host FIFO (one step in
+    flight), flush() delivers the rest, and the stream equals the HipMemcpy D2H chain's bit for bit.
+    Also reachable by JSON ("HostSink")."""
+    queue = graph.Queue.named("qg")
+    T, D, chunk, steps = 127, 2, 6000, 12
+    taps = orc.lowpass_taps(T, 0.2)
+    rng = np.random.default_rng(33)
+    iq = rng.integers(-128, 128, size=2 * chunk * steps).astype(np.int8)
+    # reference stream: the same chain ending in the D2H memcpy filter
+    conv, tail, drv = _am_chain_graph(graph, queue, taps, D)
+    ref, per_step = [], []
+    for s in range(steps):
+        conv.push(iq[2 * chunk * s: 2 * chunk * (s + 1)])
+        drv.do_filter()
+        ref.append(_read_host(graph, queue, tail))
+        per_step.append(len(ref[-1]) * 4)
+    ref = np.concatenate(ref)
+    for make in (lambda: graph.Node.host_sink(queue),
+                 lambda: graph.Node.from_json("HostSink", '{"commandQueue": "qg"}', queue)):
+        conv = graph.Node.int8_to_float(queue)
+        fir = graph.Node.fir(queue, taps, D)
+        am = graph.Node.quad_am_demod(queue)
+        sink = make()
+        drv = graph.SteppingDriver()
+        drv.connect(conv, 0, fir, 0)
+        drv.connect(fir, 0, am, 0)
+        drv.connect(am, 0, sink, 0)
+        got, delivered = [], 0
+        for s in range(steps):
+            conv.push(iq[2 * chunk * s: 2 * chunk * (s + 1)])
+            drv.do_filter()
+            delivered += sink.host_available()
+            got.append(sink.host_read(np.float32))
+            assert delivered == sum(per_step[:s]), (s, delivered)  # step s still in flight
+        sink.host_flush()
+        got.append(sink.host_read(np.float32))
+        got = np.concatenate(got)
+        assert got.tobytes() == ref.tobytes()
