@@ -15,13 +15,14 @@ run() {  # run <dir> <rocprof args...> : rocprofv3 <args> over a short bench run
   local d=$1; shift
   echo "=== $d ($(date +%T))"
   (cd /tmp && timeout -k 10 240 rocprofv3 "$@" --output-format csv -d "$OUT/$d" -o run -- \
-      python3 "$ROOT/bench.py" --workload "$WL" --steps 10 --warmup 2 --no-cpu-baseline) > "$OUT/$d.log" 2>&1
+      python3 "$ROOT/bench.py" --workload "$WL" --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline) > "$OUT/$d.log" 2>&1
   local rc=$?
   echo "=== $d rc=$rc"
   if [ $rc -ne 0 ]; then tail -n 20 "$OUT/$d.log"; exit $rc; fi
 }
 for WL in $WLS; do
-  run "${WL}_stats" --kernel-trace --stats
+  STEPS=40 run "${WL}_stats" --kernel-trace --stats
+  python3 tools/kernel_trace_summary.py "$OUT/${WL}_stats" > "$OUT/${WL}_trace_summary.txt" || exit 1
   run "${WL}_fetch" --pmc FETCH_SIZE
   run "${WL}_write" --pmc WRITE_SIZE
   python3 tools/pmc_traffic.py "$WL" "$OUT/${WL}_fetch" "$OUT/${WL}_write" "$OUT/${WL}_traffic.json" || exit 1
