@@ -234,9 +234,15 @@ class AmChainShard:
         ops.fir(self.rf_taps, self.buf, g.decimation, g.head_rf, out=self.am[: g.head_rf], am=True, int8_iq=True)
 
     def step(self):
-        """One step over the segment currently in self.seg; the audio lands in self.out."""
+        """One step over the segment currently in self.seg; the audio lands in self.out. A single
+        rank (the halo is its own history) runs the RF stage as ONE launch over [halo | segment]:
+        the halo is a multiple of D, so its outputs are the bulk's and the head's, bit for bit."""
         from . import ops
         g = self.geom
-        self.ring.step(self._bulk, self._head)
+        if g.world == 1:
+            ops.fir(self.rf_taps, self.buf, g.decimation, g.rf_outputs, out=self.am, am=True, int8_iq=True)
+            self.ring.halo.copy_(self.ring.tail)  # history carry for the next step
+        else:
+            self.ring.step(self._bulk, self._head)
         ops.fir(self.audio_taps, self.am, g.audio_decimation, g.outputs, out=self.out)
         return self.out

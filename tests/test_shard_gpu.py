@@ -116,3 +116,42 @@ def test_c5_chain_time_sharded_cascaded_halo(tmp_path, orc):
     carried, _ = orc.fir_f64(np.abs(au), (FIR_TOL * (rf_bound + am)).astype(np.float32), Da, n)
     bound = carried + FIR_TOL * audio_bound[:n] + 1e-30
     assert np.all(np.abs(got - want[:n]) <= bound)
+
+
+def test_c5_chain_single_rank_one_launch_matches_split(orc):
+    """World 1: AmChainShard runs the RF stage as one launch over [halo | segment]. Against the bulk +
+    head split the outputs may differ in the last bits (the matrix-core kernel's tiles start 360
+    outputs apart, so an output's split-K partial sums group its taps differently); both meet the
+    float64 chain within the carried tolerance."""
+    import torch
+    from gpusdr import ops
+    from gpusdr.shard import AmChainShard, ChainShardGeometry
+    T, D, Ta, Da, L = 1023, 10, 255, 20, 40_000
+    dev = torch.device("cuda", 0)
+    geom = ChainShardGeometry(0, 1, L, T, D, Ta, Da)
+    rf = torch.from_numpy(orc.lowpass_taps(T, 0.04, "blackman")).to(dev)
+    au = torch.from_numpy(orc.lowpass_taps(Ta, 0.02)).to(dev)
+    H = geom.halo
+    one = AmChainShard(geom, rf, au, dev)
+    split = AmChainShard(geom, rf, au, dev)
+    for sh in (one, split):
+        ops.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, H, out=sh.buf[: 2 * H])
+    got, ref = [], []
+    for step in range(3):
+        for sh in (one, split):
+            ops.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, H + geom.segment_start(step), L, out=sh.seg)
+        got.append(one.step().cpu().numpy().copy())
+        split.ring.step(split._bulk, split._head)
+        ops.fir(au, split.am, Da, geom.outputs, out=split.out)
+        ref.append(split.out.cpu().numpy().copy())
+    got, ref = np.concatenate(got), np.concatenate(ref)
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-7)
+    padded = orc.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, H + 3 * L)
+    x = orc.int8_to_float(padded).view(np.complex64)
+    y, rf_bound = orc.fir_f64(orc.lowpass_taps(T, 0.04, "blackman"), x, D)
+    am = np.abs(y)
+    want, audio_bound = orc.fir_f64(orc.lowpass_taps(Ta, 0.02), am.astype(np.float32), Da)
+    n = len(got)
+    carried, _ = orc.fir_f64(np.abs(orc.lowpass_taps(Ta, 0.02)), (FIR_TOL * (rf_bound + am)).astype(np.float32), Da, n)
+    for out in (got, ref):
+        assert np.all(np.abs(out - want[:n]) <= carried + FIR_TOL * audio_bound[:n] + 1e-30)
