@@ -236,10 +236,11 @@ class AmChainSharded:
         nxt = self.slots[(self.cur + 1) % self.n_slots]
         if ev is not None:
             ev[0].record()
-        sh.step()
+        # one rank: the history goes straight into the next slot's halo
+        sh.step(carry_to=nxt.ring.halo if g.world == 1 else None)
         if ev is not None:
             ev[1].record()
-        if self.n_slots > 1 and (g.world == 1 or g.rank == 0):
+        if self.n_slots > 1 and g.world > 1 and g.rank == 0:
             nxt.ring.halo.copy_(sh.ring.halo)
         self.cur = (self.cur + 1) % self.n_slots
 

@@ -233,15 +233,16 @@ class AmChainShard:
         g = self.geom
         ops.fir(self.rf_taps, self.buf, g.decimation, g.head_rf, out=self.am[: g.head_rf], am=True, int8_iq=True)
 
-    def step(self):
+    def step(self, carry_to=None):
         """One step over the segment currently in self.seg; the audio lands in self.out. A single
-        rank (the halo is its own history) runs the RF stage as ONE launch over [halo | segment]:
-        the halo is a multiple of D, so its outputs are the bulk's and the head's, bit for bit."""
+        rank (the halo is its own history) runs the RF stage as ONE launch over [halo | segment]
+        (the halo is a multiple of D: the same outputs as the bulk and head launches) and copies the
+        segment's tail to `carry_to` (default: its own halo), the next step's history."""
         from . import ops
         g = self.geom
         if g.world == 1:
             ops.fir(self.rf_taps, self.buf, g.decimation, g.rf_outputs, out=self.am, am=True, int8_iq=True)
-            self.ring.halo.copy_(self.ring.tail)  # history carry for the next step
+            (self.ring.halo if carry_to is None else carry_to).copy_(self.ring.tail)
         else:
             self.ring.step(self._bulk, self._head)
         ops.fir(self.audio_taps, self.am, g.audio_decimation, g.outputs, out=self.out)
