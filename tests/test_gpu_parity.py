@@ -690,3 +690,37 @@ def test_fm_demod_reference_entry(ops, orc):
     gain = float(f32(f32(rf_rate) / f32(D)) / (f32(2.0) * f32(np.pi) * f32(dev_hz) * f32(5)))
     ref = _host(ops.fm_front(td, xd, D, n_out, step * first, step, gain))
     assert got.tobytes() == ref.tobytes()
+
+
+def test_zero_length_calls_are_no_ops(ops):
+    """Every entry point called with 0 outputs / elements (an empty chunk, as a SteppingDriver step
+    with nothing buffered produces) succeeds, launches nothing and writes nothing - through the
+    C ABI directly, null data pointers included (Fir.cpp:221-223 returns before the kernel when
+    nOut is 0)."""
+    import ctypes
+
+    import torch
+    from gpusdr._native import lib
+    L = lib()
+    sentinel = torch.full((64,), 7.0, dtype=torch.float32, device="cuda")
+    x = torch.zeros(64, dtype=torch.complex64, device="cuda")
+    taps = torch.ones(8, dtype=torch.float32, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    calls = []
+    for name in sorted(set(ops._FIR_ENTRY.values())):
+        calls.append((name, lambda f, o: f(1, taps.data_ptr(), 8, x.data_ptr(), o, 0, 0, stream)))
+        calls.append((name + "(null)", lambda f, o: f(1, None, 8, None, None, 0, 0, stream)))
+    for name in sorted(set(ops._MIX_ENTRY.values())):
+        calls.append((name, lambda f, o: f(2, taps.data_ptr(), 8, x.data_ptr(), ctypes.c_double(0.0),
+                                           ctypes.c_double(0.1), o, 0, 0, stream)))
+    torch.cuda.synchronize()
+    for name, call in calls:
+        fn = getattr(L, name.split("(")[0])
+        assert call(fn, sentinel.data_ptr()) == 0, name
+    assert L.gsdrQuadAmDemod(x.data_ptr(), sentinel.data_ptr(), 0, 0, stream) == 0
+    assert L.gsdrInt8ToNormFloat(None, None, 0, 0, stream) == 0
+    assert L.gsdrMultiplyCC(None, None, None, 0, 0, stream) == 0
+    assert L.gsdrQuadFmDemod(None, None, ctypes.c_float(1.0), 0, 0, stream) == 0
+    assert L.gsdrCosineF(ctypes.c_float(0.0), ctypes.c_float(1.0), None, 0, 0, stream) == 0
+    torch.cuda.synchronize()
+    assert torch.all(sentinel == 7.0)
