@@ -113,6 +113,36 @@ def test_fft_fir_large_stream_properties(ops, orc):
     assert np.max(np.abs(am - am_mfma)) <= 2 * FIR_TOL * 0.45 * np.abs(taps).sum() * 1.01
 
 
+def test_fft_fir_full_c3_size(ops, orc):
+    """BASELINE's C3 at full size (2^28 - 6 cf32 samples, 1023 taps, D = 10, AM): 4 000 outputs
+    sampled over the whole stream - the first and last, both sides of FFT block boundaries and
+    random ones - against float64 on their own windows (gathered on the GPU), and no block took the
+    direct-form fallback on this signal."""
+    import torch
+    T, D = 1023, 10
+    n_in = (1 << 28) - (1 << 28) % D
+    n_out = (n_in - T) // D + 1
+    x_d = ops.synth_wideband_cf32(0xC3, 0.013, 0.31, 0, n_in)
+    taps = orc.lowpass_taps(T, 0.04, "blackman")
+    ops.fft_direct_blocks(0, reset=True)
+    am = ops.fir(_dev(taps), x_d, D, n_out, am=True)
+    torch.cuda.synchronize()
+    assert ops.fft_direct_blocks(0, reset=True) == 0
+    rng = np.random.default_rng(28)
+    V = 512 - (T + D - 1) // D + 1  # outputs per FFT block
+    edges = np.arange(V, n_out, V * 977)
+    ks = np.unique(np.concatenate([[0, 1, n_out - 2, n_out - 1], edges - 1, edges,
+                                   rng.integers(0, n_out, 4000 - 2 * len(edges) - 4)]))
+    ks = ks[ks < n_out]
+    idx = torch.from_numpy(ks * D).cuda()[:, None] + torch.arange(T, device="cuda")[None, :]
+    windows = x_d[idx].cpu().numpy()          # (len(ks), T) complex64
+    got = am[torch.from_numpy(ks).cuda()].cpu().numpy()
+    y = windows.astype(np.complex128) @ taps.astype(np.float64)
+    bound = np.abs(windows).astype(np.float64) @ np.abs(taps.astype(np.float64))
+    err = np.abs(got - np.abs(y))
+    assert np.all(err <= FIR_TOL * bound), float(np.max(err / bound))
+
+
 class _Policy:
     def __init__(self, ops, flags):
         self.ops, self.flags = ops, flags
@@ -201,3 +231,44 @@ def test_fft_fir_int8_alignment(ops, orc, off):
     xc = orc.int8_to_float(iq[off:]).view(np.complex64)
     y64, bound = orc.fir_f64(taps, xc, D, n_out)
     _check(y, y64, bound, ("i8-align", off))
+
+
+def test_full_c2_and_c5_sizes(ops, orc):
+    """BASELINE's C2 (20 M int8 IQ, 127 taps, D = 1, AM; one launch with the history carry) and the
+    C5 RF + audio chain at full size (125 M int8 IQ, 1023 taps D = 10 -> AM -> 255 taps D = 20):
+    sampled outputs against float64 on their own windows gathered on the GPU."""
+    import torch
+    rng = np.random.default_rng(25)
+    # C2
+    T, D, n = 127, 1, 20_000_000
+    iq = ops.synth_iq_int8(0x5EED, 20e6, 1e3, 1.5e6, 0, n + T - 1)
+    taps = orc.lowpass_taps(T, 0.1)
+    am = torch.empty(n, dtype=torch.float32, device="cuda")
+    carry = torch.empty(2 * (T - 1), dtype=torch.int8, device="cuda")
+    ops.fir_am_i8_carry(_dev(taps), iq, D, n, am, carry)
+    ks = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, 3000)]))
+    idx = (torch.from_numpy(2 * ks).cuda()[:, None] + torch.arange(2 * T, device="cuda")[None, :])
+    w = orc.int8_to_float(iq[idx].cpu().numpy().reshape(-1)).view(np.complex64).reshape(len(ks), T)
+    y = w.astype(np.complex128) @ taps.astype(np.float64)
+    bound = np.abs(w).astype(np.float64) @ np.abs(taps.astype(np.float64))
+    assert np.all(np.abs(am[torch.from_numpy(ks).cuda()].cpu().numpy() - np.abs(y)) <= FIR_TOL * bound)
+    assert torch.equal(carry, iq[2 * n: 2 * (n + T - 1)])  # the next call's history
+    # C5
+    T, D, Ta, Da, n_in = 1023, 10, 255, 20, 125_000_000
+    iq = ops.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, n_in)
+    rf, au = orc.lowpass_taps(T, 0.04, "blackman"), orc.lowpass_taps(Ta, 0.02)
+    n_rf = (n_in - T) // D + 1
+    amd = ops.fir(_dev(rf), iq, D, n_rf, am=True, int8_iq=True)
+    n_au = (n_rf - Ta) // Da + 1
+    aud = ops.fir(_dev(au), amd, Da, n_au)
+    ks = np.unique(np.concatenate([[0, n_au - 1], rng.integers(0, n_au, 300)]))
+    span = (Ta - 1) * D + T  # input samples under one audio output
+    idx = (torch.from_numpy(2 * ks * Da * D).cuda()[:, None] + torch.arange(2 * span, device="cuda")[None, :])
+    w = orc.int8_to_float(iq[idx].cpu().numpy().reshape(-1)).view(np.complex64).reshape(len(ks), span)
+    got = aud[torch.from_numpy(ks).cuda()].cpu().numpy()
+    for r, k in enumerate(ks):
+        y, rf_bound = orc.fir_f64(rf, w[r], D, Ta)
+        a = np.abs(y)
+        want, audio_bound = orc.fir_f64(au, a.astype(np.float32), Da, 1)
+        carried, _ = orc.fir_f64(np.abs(au), (FIR_TOL * (rf_bound + a)).astype(np.float32), Da, 1)
+        assert abs(got[r] - want[0]) <= carried[0] + FIR_TOL * audio_bound[0] + 1e-30, k
