@@ -575,6 +575,140 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   }
 }
 
+// ---- D = 1: eight output phases per block from eight shared input-phase spectra -----------------
+// With k = 8m + r and j = 8q + p (p, r < 8), y[8m + r] = sum_p sum_q h_p[q] x_{(p+r) mod 8}[m + q + c],
+// c = (p + r >= 8), x_t[n] = x[8n + t], h_p[q] = h[8q + p]: each output phase r is an 8-phase
+// polyphase correlation of the SAME input phases, some advanced by one row. A block of 512 rows (8
+// samples each) is transformed once per input phase (8 forward FFTs, spectra kept in registers in
+// place of the rows); output phase r is Y_r = sum_{p < 8-r} X_{p+r} G_p + w^k sum_{p >= 8-r}
+// X_{p+r-8} G_p (w^k = exp(+2 pi i k / 512): the one-row advance) and one inverse FFT, valid for
+// m < V = 512 - Q. Per block 8 V outputs for 16 FFTs - against D x (one FFT per phase) + 1 per V
+// outputs at D >= 2 - so the long D = 1 filter (C4: 1023 taps) runs at a few hundred flops per
+// sample instead of 4 T.
+constexpr int kOmega = 512;  // w^k table, per-lane float4 pairs like G
+
+template <int EPI>
+__device__ void directBlockD1(const Args& a, int64_t b, int l) {
+  const int64_t k0 = b * (int64_t)a.V * 8;  // first output of the block
+  const int64_t left = a.nOut - k0;
+  const int nv = __builtin_amdgcn_readfirstlane((int)(left < 8 * a.V ? left : 8 * a.V));
+  for (int i = l; i < nv; i += 64) {
+    float re = 0.0f, im = 0.0f;
+    for (int t0 = 0; t0 < a.T; t0 += 64) {  // blocked sums, as the other direct forms
+      const int t1 = t0 + 64 < a.T ? t0 + 64 : a.T;
+      float pr = 0.0f, pi = 0.0f;
+      for (int t = t0; t < t1; ++t) {
+        const f2 x = reinterpret_cast<const f2*>(a.in)[k0 + i + t];
+        pr = fmaf(a.taps[t], x.x, pr);
+        pi = fmaf(a.taps[t], x.y, pi);
+      }
+      re += pr;
+      im += pi;
+    }
+    if (EPI == kAm)
+      reinterpret_cast<float*>(a.out)[k0 + i] = amEnvelope(f2{re, im});
+    else
+      reinterpret_cast<f2*>(a.out)[k0 + i] = f2{re, im};
+  }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(kThreads) firFftD1Kernel(Args a) {
+  constexpr int D = 8;  // input phases (rows of 8 samples)
+  extern __shared__ __attribute__((aligned(16))) f2 lds[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  f2* twAll = lds + D * 8 * 64;
+  f2* omegaAll = twAll + kTw + kWaves * scratchComplex<D>(kCf32);
+  Lds L;
+  L.g = reinterpret_cast<f4*>(lds);
+  L.tw = reinterpret_cast<const f4*>(twAll) + l;
+  L.scratch = twAll + kTw + w * scratchComplex<D>(kCf32);
+  for (int n = threadIdx.x; n < kOmega; n += kThreads) {
+    // complex n = ((d / 2) 64 + lane) 2 + (d & 1); layout F: lane = 8 k0 + c holds k0 + 8 c + 64 d
+    const int lane = (n >> 1) & 63, d = 2 * (n >> 7) + (n & 1);
+    const int k = (lane >> 3) + 8 * (lane & 7) + 64 * d;
+    double sn, cs;
+    sincospi(2.0 * k / kM, &sn, &cs);
+    omegaAll[n] = f2{(float)cs, (float)sn};
+  }
+  buildTables<D, kCf32>(a, twAll, L, w, l);  // (its barriers also publish the w^k table)
+  const f4* omega = reinterpret_cast<const f4*>(omegaAll) + l;
+  if (w >= kWaves / 2) {
+    for (int i = 0; i < GSDR_FFT_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+  const int64_t stride = (int64_t)gridDim.x * kWaves;
+  for (int64_t b = (int64_t)blockIdx.x * kWaves + w; b < a.nBlocks; b += stride) {
+    Rows<D, kCf32> R;
+    loadRows<D>(a, b, R, L.scratch, l);
+    if (blockNeedsDirect<D, kCf32>(a, R, b, l)) {
+      if (l == 0) atomicAdd(&gDirectBlocks, 1ull);
+      directBlockD1<EPI>(a, b, l);
+      continue;
+    }
+    // the eight input-phase spectra, in place of the rows
+    f2 X[D][8];
+#pragma unroll
+    for (int p = 0; p < D; p += 2) {
+      f2 z[2][8];
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) z[n][j] = R.point(j, p + n);
+      fftFwd<2>(z, L, l);
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int d = 0; d < 8; ++d) X[p + n][d] = z[n][d];
+    }
+    const int64_t row0 = b * (int64_t)a.V;
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      f2 acc[1][8], sh[8];
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        acc[0][d] = f2{0.0f, 0.0f};
+        sh[d] = f2{0.0f, 0.0f};
+      }
+#pragma unroll
+      for (int p = 0; p < D; ++p) {
+        f2 g[8];
+#pragma unroll
+        for (int d = 0; d < 8; d += 2) {
+          const f4 v = L.g[(p * 4 + d / 2) * 64 + l];
+          g[d] = f2{v.x, v.y};
+          g[d + 1] = f2{v.z, v.w};
+        }
+        const int t = p + r;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+          if (t < D) acc[0][d] = cmac(X[t][d], g[d], acc[0][d]);
+          else sh[d] = cmac(X[t - D][d], g[d], sh[d]);
+        }
+      }
+      if (r > 0) {  // the one-row advance of the wrapped phases
+#pragma unroll
+        for (int d = 0; d < 8; d += 2) {
+          const f4 v = omega[(d / 2) * 64];
+          acc[0][d] = cmac(sh[d], f2{v.x, v.y}, acc[0][d]);
+          acc[0][d + 1] = cmac(sh[d + 1], f2{v.z, v.w}, acc[0][d + 1]);
+        }
+      }
+      ifft512(acc, L, l);
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        const int m = l + 64 * h;
+        const int64_t k = 8 * (row0 + m) + r;
+        if (m < a.V && k < a.nOut) {
+          if (EPI == kAm)
+            reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc[0][h]);
+          else
+            reinterpret_cast<f2*>(a.out)[k] = acc[0][h];
+        }
+      }
+    }
+  }
+}
+
 }  // namespace fftfir
 
 // ------------------------------------------------------------------------------------ host
@@ -607,6 +741,24 @@ hipError_t launchD(fftfir::Args a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+template <int EPI>
+hipError_t launchD1(fftfir::Args a, hipStream_t stream) {
+  using namespace fftfir;
+  auto kernel = firFftD1Kernel<EPI>;
+  const size_t lds = ldsBytes<8, kCf32>() + (size_t)kOmega * sizeof(f2);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int64_t maxGroups = cuCount();
+  int64_t groups = (a.nBlocks + kWaves - 1) / kWaves;
+  if (groups > maxGroups) groups = maxGroups;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)groups), dim3(kThreads), lds, stream, a);
+  return hipGetLastError();
+}
+
 template <int IN, int EPI>
 hipError_t launchFft(fftfir::Args a, size_t D, hipStream_t stream) {
   switch (D) {
@@ -625,6 +777,10 @@ hipError_t launchFft(fftfir::Args a, size_t D, hipStream_t stream) {
 // at least 64 outputs per block, and the loads' alignment (cf32: 16-byte input; int8 IQ: 4-byte).
 bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int8Iq) {
   const size_t D = decimation < 1 ? 1 : decimation;
+  if (D == 1) {  // cf32: eight output phases per block (firFftD1Kernel), up to 3 584 taps
+    const size_t Q = (tapCount + 7) / 8;
+    return !int8Iq && tapCount >= 256 && Q <= (size_t)fftfir::kM - 64 && ((uintptr_t)in & 15) == 0;
+  }
   if (!(D == 2 || D == 4 || D == 6 || D == 8 || D == 10)) return false;
   const size_t Q = (tapCount + D - 1) / D;
   if (tapCount < 256 || Q > (size_t)fftfir::kM - 63) return false;
@@ -642,6 +798,23 @@ hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t t
   using namespace fftfir;
   if (nOut == 0) return hipSuccess;
   const size_t D = decimation < 1 ? 1 : decimation;
+  if (D == 1) {
+    if (int8Iq) return hipErrorInvalidValue;
+    Args a{};
+    a.in = in;
+    a.taps = taps;
+    a.out = out;
+    a.nOut = (int64_t)nOut;
+    a.T = (int32_t)tapCount;
+    a.Q = (int32_t)((tapCount + 7) / 8);
+    a.V = kM - a.Q;  // rows per block: the one-row advance costs one
+    a.inBytes = (int64_t)(nOut - 1 + tapCount) * 8;
+    a.nBlocks = ((int64_t)nOut + 8 * (int64_t)a.V - 1) / (8 * (int64_t)a.V);
+    a.inRows = (int64_t)((nOut - 1 + tapCount) / 8);
+    a.inScale = 1.0f;
+    a.guardRatio = gFftGuard.load(std::memory_order_relaxed);
+    return epi == kEpiAm ? launchD1<kAm>(a, stream) : launchD1<kComplex>(a, stream);
+  }
   Args a{};
   a.in = in;
   a.taps = taps;

@@ -64,7 +64,10 @@ FFT_CASES = [("c64", 1023, 10, 20000), ("c64", 1023, 10, 1), ("c64", 1023, 10, 4
              ("c64-noise", 1023, 10, 30000), ("c64", 256, 2, 5000), ("c64-noise", 511, 4, 7777),
              ("c64", 600, 6, 3001), ("c64-noise", 2000, 8, 4096), ("c64", 4000, 10, 999),
              ("i8", 1023, 10, 20000), ("i8", 1023, 10, 1), ("i8", 300, 2, 5000), ("i8", 700, 4, 12345),
-             ("i8", 1000, 8, 2222)]
+             ("i8", 1000, 8, 2222),
+             # D = 1 (firFftD1Kernel: 8 output phases of 512 - ceil(T/8) rows per block)
+             ("c64", 1023, 1, 20000), ("c64", 1023, 1, 1), ("c64", 1023, 1, 3072), ("c64", 1023, 1, 3073),
+             ("c64-noise", 256, 1, 9999), ("c64", 3584, 1, 5000), ("c64-noise", 2000, 1, 7001)]
 
 
 @pytest.mark.parametrize("kind,T,D,n_out", FFT_CASES)
@@ -200,9 +203,10 @@ def test_fft_fir_nonfinite_stays_local(ops, orc):
     _check(y[~bad], y64[~bad], bound[~bad], "nonfinite")
 
 
-def test_fft_fir_guard_zero_is_direct(ops, orc):
+@pytest.mark.parametrize("D,per_block", [(10, 410), (1, 8 * 384)])
+def test_fft_fir_guard_zero_is_direct(ops, orc, D, per_block):
     """Guard ratio 0 forces every block into the direct form (the fallback path in isolation)."""
-    T, D, n_out = 1023, 10, 5000
+    T, n_out = 1023, 5000
     n_in = (n_out - 1) * D + T
     x = _signal("c64", n_in, 1, orc)
     taps = orc.lowpass_taps(T, 0.04, "blackman")
@@ -213,7 +217,7 @@ def test_fft_fir_guard_zero_is_direct(ops, orc):
         direct = ops.fft_direct_blocks(reset=True)
     finally:
         ops.set_fft_guard(prev)
-    assert direct == -(-n_out // 410)
+    assert direct == -(-n_out // per_block)
     y64, bound = orc.fir_f64(taps, x, D, n_out)
     _check(y, y64, bound, "guard0")
 
