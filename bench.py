@@ -257,12 +257,16 @@ class AmChainSharded:
 def kernel_compute(cls, n_out, T, D):
     """(kind, flops per launch, peak TFLOP/s) of the FIR kernel family `cls` for n_out outputs."""
     if cls == "fft":
+        fft = 5 * 512 * 9  # nominal 5 N log2 N per 512-point FFT
+        kind = "fp32 FFT fast convolution (polyphase overlap-save, 512-point FFTs; nominal 5 N log2 N)"
+        if D == 1:  # firFftD1Kernel: 8 input-phase FFTs, 8 x 8 spectral MACs, 8 inverse FFTs per block
+            V = 512 - -(-T // 8)
+            blocks = -(-n_out // (8 * V))
+            return kind, blocks * (8 * fft + 64 * 512 * 8 + 8 * fft), FP32_PEAK_TFLOPS
         Q = -(-T // D)
         V = 512 - Q + 1
         blocks = -(-n_out // V)
-        fft = 5 * 512 * 9  # nominal 5 N log2 N per 512-point FFT
-        return ("fp32 FFT fast convolution (polyphase overlap-save, 512-point FFTs; nominal 5 N log2 N)",
-                blocks * (D * fft + D * 512 * 8 + fft), FP32_PEAK_TFLOPS)
+        return kind, blocks * (D * fft + D * 512 * 8 + fft), FP32_PEAK_TFLOPS
     if cls == "i8-mfma":
         s = (T + 62) // 32  # K-blocks of 32: K = 32 S >= T + 31
         return ("f16 MFMA (2 tap limbs, fp32 accumulate)", n_out * 2 * 2 * 32 * s * 2, F16_PEAK_TFLOPS)
@@ -422,8 +426,8 @@ def kernel_name(chain):
                 "HIP events around the whole step)")
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"
-    body = {"fft": "firFftKernel", "i8-mfma": "firI8MfmaKernel", "i8-dec-mfma": "firI8WsKernel",
-            "cf-mfma": "firCfWsKernel", "valu": "firLdsKernel"}[chain.kernel_class]
+    body = {"fft": "firFftD1Kernel" if chain.D == 1 else "firFftKernel", "i8-mfma": "firI8MfmaKernel",
+            "i8-dec-mfma": "firI8WsKernel", "cf-mfma": "firCfWsKernel", "valu": "firLdsKernel"}[chain.kernel_class]
     return f"{entry} ({body})"
 
 
