@@ -61,6 +61,28 @@ __global__ void chunkRead(const char* x, size_t nBlocks, float* sink) {
   if (acc == 12345.678f) sink[0] = acc;
 }
 
+// chunk reads with the FFT kernel's geometry: block stride STRIDE bytes (32800 = 410 rows x 80 B),
+// 40 KB per block; ROT: wave-dependent rotation of the 40 instructions' issue order
+template <int W, int STRIDE, int ROT>
+__global__ void chunkReadV(const char* x, size_t nBlocks, float* sink) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  float acc = 0.0f;
+  for (size_t b = blockIdx.x * (size_t)W + w; b < nBlocks; b += (size_t)gridDim.x * W) {
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + b * STRIDE), (short)0, 40960, 0x00020000);
+    float4 v[40];
+    const int rot = ROT ? (int)(b % 8) * 5 : 0;
+#pragma unroll
+    for (int i = 0; i < 40; ++i) {
+      int ii = i + rot;
+      ii = ii >= 40 ? ii - 40 : ii;
+      v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (ii * 64 + l) * 16, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < 40; ++i) acc += v[i].x + v[i].w;
+  }
+  if (acc == 12345.678f) sink[0] = acc;
+}
+
 void readBw(void* x, size_t bytes) {
   float* sink;
   hipMalloc(&sink, 64);
@@ -91,6 +113,11 @@ void readBw(void* x, size_t bytes) {
   timeit("chunk 8 waves nt", [&] { chunkRead<8, 2><<<256, 512>>>((const char*)x, nb, sink); });
   timeit("chunk 4 waves", [&] { chunkRead<4, 0><<<256, 256>>>((const char*)x, nb, sink); });
   timeit("chunk 16 waves", [&] { chunkRead<16, 0><<<256, 1024>>>((const char*)x, nb, sink); });
+  const size_t nb2 = (bytes - 40960) / 32800;
+  timeit("chunkV 8w stride32800", [&] { chunkReadV<8, 32800, 0><<<256, 512>>>((const char*)x, nb2, sink); });
+  timeit("chunkV 8w stride32800 rot", [&] { chunkReadV<8, 32800, 1><<<256, 512>>>((const char*)x, nb2, sink); });
+  timeit("chunkV 8w stride40960 rot", [&] { chunkReadV<8, 40960, 1><<<256, 512>>>((const char*)x, nb, sink); });
+  timeit("chunkV 8w stride41216", [&] { chunkReadV<8, 41216, 0><<<256, 512>>>((const char*)x, (bytes - 40960) / 41216, sink); });
   hipFree(sink);
 }
 
