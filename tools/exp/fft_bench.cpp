@@ -83,6 +83,23 @@ __global__ void chunkReadV(const char* x, size_t nBlocks, float* sink) {
   if (acc == 12345.678f) sink[0] = acc;
 }
 
+// the same 8 blocks per workgroup, but read as one interleaved sweep: instruction i of wave w
+// loads 1 KB piece 8 i + w of the workgroup's contiguous 8-block region
+__global__ void chunkReadSweep(const char* x, size_t nGroups, float* sink) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  float acc = 0.0f;
+  for (size_t g = blockIdx.x; g < nGroups; g += gridDim.x) {
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + g * 8 * 40960), (short)0, 8 * 40960, 0x00020000);
+    float4 v[40];
+#pragma unroll
+    for (int i = 0; i < 40; ++i)
+      v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * 8 + w) * 64 + l) * 16, 0, 0));
+#pragma unroll
+    for (int i = 0; i < 40; ++i) acc += v[i].x + v[i].w;
+  }
+  if (acc == 12345.678f) sink[0] = acc;
+}
+
 void readBw(void* x, size_t bytes) {
   float* sink;
   hipMalloc(&sink, 64);
@@ -113,6 +130,7 @@ void readBw(void* x, size_t bytes) {
   timeit("chunk 8 waves nt", [&] { chunkRead<8, 2><<<256, 512>>>((const char*)x, nb, sink); });
   timeit("chunk 4 waves", [&] { chunkRead<4, 0><<<256, 256>>>((const char*)x, nb, sink); });
   timeit("chunk 16 waves", [&] { chunkRead<16, 0><<<256, 1024>>>((const char*)x, nb, sink); });
+  timeit("sweep 8 waves (8 blocks/WG)", [&] { chunkReadSweep<<<256, 512>>>((const char*)x, bytes / (8 * 40960), sink); });
   const size_t nb2 = (bytes - 40960) / 32800;
   timeit("chunkV 8w stride32800", [&] { chunkReadV<8, 32800, 0><<<256, 512>>>((const char*)x, nb2, sink); });
   timeit("chunkV 8w stride32800 rot", [&] { chunkReadV<8, 32800, 1><<<256, 512>>>((const char*)x, nb2, sink); });
