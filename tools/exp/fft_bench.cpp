@@ -48,7 +48,7 @@ __global__ void streamRead(const f4v* x, size_t n4, float* sink) {
 // dwordx4 instructions) then consumes them; W waves per workgroup, one workgroup per CU
 template <int W, int AUX>
 __global__ void chunkRead(const char* x, size_t nBlocks, float* sink) {
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   float acc = 0.0f;
   for (size_t b = blockIdx.x * (size_t)W + w; b < nBlocks; b += (size_t)gridDim.x * W) {
     __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + b * 40960), (short)0, 40960, 0x00020000);
@@ -65,7 +65,7 @@ __global__ void chunkRead(const char* x, size_t nBlocks, float* sink) {
 // 40 KB per block; ROT: wave-dependent rotation of the 40 instructions' issue order
 template <int W, int STRIDE, int ROT>
 __global__ void chunkReadV(const char* x, size_t nBlocks, float* sink) {
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   float acc = 0.0f;
   for (size_t b = blockIdx.x * (size_t)W + w; b < nBlocks; b += (size_t)gridDim.x * W) {
     __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + b * STRIDE), (short)0, 40960, 0x00020000);
@@ -86,7 +86,7 @@ __global__ void chunkReadV(const char* x, size_t nBlocks, float* sink) {
 // the same 8 blocks per workgroup, but read as one interleaved sweep: instruction i of wave w
 // loads 1 KB piece 8 i + w of the workgroup's contiguous 8-block region
 __global__ void chunkReadSweep(const char* x, size_t nGroups, float* sink) {
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   float acc = 0.0f;
   for (size_t g = blockIdx.x; g < nGroups; g += gridDim.x) {
     __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + g * 8 * 40960), (short)0, 8 * 40960, 0x00020000);
@@ -94,6 +94,43 @@ __global__ void chunkReadSweep(const char* x, size_t nGroups, float* sink) {
 #pragma unroll
     for (int i = 0; i < 40; ++i)
       v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * 8 + w) * 64 + l) * 16, 0, 0));
+#pragma unroll
+    for (int i = 0; i < 40; ++i) acc += v[i].x + v[i].w;
+  }
+  if (acc == 12345.678f) sink[0] = acc;
+}
+
+// per-wave chunks with the 40 loads issued at raised wave priority (PRIO = 1: s_setprio 3 around
+// the issue, so a wave tends to issue its whole block before its SIMD partner interleaves)
+template <int W, int PRIO>
+__global__ void chunkReadPrio(const char* x, size_t nBlocks, float* sink) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  float acc = 0.0f;
+  for (size_t b = blockIdx.x * (size_t)W + w; b < nBlocks; b += (size_t)gridDim.x * W) {
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + b * 40960), (short)0, 40960, 0x00020000);
+    float4 v[40];
+    if (PRIO) __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+    for (int i = 0; i < 40; ++i) v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (i * 64 + l) * 16, 0, 0));
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int i = 0; i < 40; ++i) acc += v[i].x + v[i].w;
+  }
+  if (acc == 12345.678f) sink[0] = acc;
+}
+
+// sweeps shared by groups of G waves: the G waves of a group read their G-block region
+// interleaved (instruction i of member m loads piece G i + m), 8 / G groups per workgroup
+template <int G>
+__global__ void chunkReadSweepG(const char* x, size_t nRegions, float* sink) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63, grp = w / G, m = w % G;
+  float acc = 0.0f;
+  for (size_t r = blockIdx.x * (size_t)(8 / G) + grp; r < nRegions; r += (size_t)gridDim.x * (8 / G)) {
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + r * G * 40960), (short)0, G * 40960, 0x00020000);
+    float4 v[40];
+#pragma unroll
+    for (int i = 0; i < 40; ++i)
+      v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * G + m) * 64 + l) * 16, 0, 0));
 #pragma unroll
     for (int i = 0; i < 40; ++i) acc += v[i].x + v[i].w;
   }
@@ -131,6 +168,12 @@ void readBw(void* x, size_t bytes) {
   timeit("chunk 4 waves", [&] { chunkRead<4, 0><<<256, 256>>>((const char*)x, nb, sink); });
   timeit("chunk 16 waves", [&] { chunkRead<16, 0><<<256, 1024>>>((const char*)x, nb, sink); });
   timeit("sweep 8 waves (8 blocks/WG)", [&] { chunkReadSweep<<<256, 512>>>((const char*)x, bytes / (8 * 40960), sink); });
+  timeit("chunk 8 waves setprio", [&] { chunkReadPrio<8, 1><<<256, 512>>>((const char*)x, nb, sink); });
+  timeit("chunk 8 waves 2 WG/CU", [&] { chunkRead<8, 0><<<512, 512>>>((const char*)x, nb, sink); });
+  timeit("sweep groups of 2 waves", [&] { chunkReadSweepG<2><<<256, 512>>>((const char*)x, bytes / (2 * 40960), sink); });
+  timeit("sweep groups of 4 waves", [&] { chunkReadSweepG<4><<<256, 512>>>((const char*)x, bytes / (4 * 40960), sink); });
+  timeit("sweep groups of 8 waves", [&] { chunkReadSweepG<8><<<256, 512>>>((const char*)x, bytes / (8 * 40960), sink); });
+  timeit("sweep 8 waves x2 WG/CU", [&] { chunkReadSweepG<8><<<512, 512>>>((const char*)x, bytes / (8 * 40960), sink); });
   const size_t nb2 = (bytes - 40960) / 32800;
   timeit("chunkV 8w stride32800", [&] { chunkReadV<8, 32800, 0><<<256, 512>>>((const char*)x, nb2, sink); });
   timeit("chunkV 8w stride32800 rot", [&] { chunkReadV<8, 32800, 1><<<256, 512>>>((const char*)x, nb2, sink); });
@@ -141,7 +184,8 @@ void readBw(void* x, size_t bytes) {
 
 int main() {
   struct Shape { const char* name; size_t n, T, D; bool i8; } shapes[] = {{"c3", (1u << 28) - 6, 1023, 10, false},
-                                                                          {"c5rf", 125000000, 1023, 10, true}};
+                                                                          {"c5rf", 125000000, 1023, 10, true},
+                                                                          {"c4", (1u << 27), 1023, 1, false}};
   struct V { const char* name; LaunchFn fn; } vars[] = {VARIANT_TABLE};
   const int nv = sizeof(vars) / sizeof(vars[0]);
   hipEvent_t e0, e1;
