@@ -259,7 +259,7 @@ def kernel_compute(cls, n_out, T, D):
     if cls == "fft":
         fft = 5 * 512 * 9  # nominal 5 N log2 N per 512-point FFT
         kind = "fp32 FFT fast convolution (polyphase overlap-save, 512-point FFTs; nominal 5 N log2 N)"
-        if D == 1:  # firFftD1Kernel: 8 input-phase FFTs, 8 x 8 spectral MACs, 8 inverse FFTs per block
+        if D == 1:  # firFftD1PfKernel: 8 input-phase FFTs, 8 x 8 spectral MACs, 8 inverse FFTs per block
             V = 512 - -(-T // 8)
             blocks = -(-n_out // (8 * V))
             return kind, blocks * (8 * fft + 64 * 512 * 8 + 8 * fft), FP32_PEAK_TFLOPS
@@ -426,7 +426,7 @@ def kernel_name(chain):
                 "HIP events around the whole step)")
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"
-    body = {"fft": "firFftD1Kernel" if chain.D == 1 else "firFftKernel", "i8-mfma": "firI8MfmaKernel",
+    body = {"fft": "firFftD1PfKernel" if chain.D == 1 else "firFftKernel", "i8-mfma": "firI8MfmaKernel",
             "i8-dec-mfma": "firI8WsKernel", "cf-mfma": "firCfWsKernel", "valu": "firLdsKernel"}[chain.kernel_class]
     return f"{entry} ({body})"
 

@@ -293,9 +293,9 @@ constexpr size_t ldsBytes() {
 }
 
 // Prologue: the twiddle tables and G_p = inScale * conj(DFT_512(h_p)) / 512 in layout F.
-template <int D, int IN>
+template <int D, int IN, int NW = kWaves>
 __device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l) {
-  for (int n = threadIdx.x; n < kTw; n += kThreads) {
+  for (int n = threadIdx.x; n < kTw; n += NW * kWave) {
     // complex n = ((stage 4 + kp) 64 + lane) 2 + (k & 1), k = 2 kp + (n & 1), r = k + 1
     const int stage = n >> 9, kp = (n >> 7) & 3, lane = (n >> 1) & 63, r = 2 * kp + (n & 1) + 1;
     const int lo = lane & 7, hi = lane >> 3;
@@ -312,7 +312,7 @@ __device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l
   }
   __syncthreads();
   const float sc = a.inScale / (float)kM;
-  for (int p = w; p < D; p += kWaves) {
+  for (int p = w; p < D; p += NW) {
     f2 z[1][8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -352,6 +352,26 @@ struct Rows<D, kI8> {
   }
 };
 
+// Row group j of the block as loaded (16-byte unit 64 i + l of the group in R.v[j][2i..2i+1]) ->
+// rows (R.v[j][p] = x[(l + 64 j) D + p]) through the wave's scratch.
+template <int D>
+__device__ __forceinline__ void transposeRows(Rows<D, kCf32>& R, f2* s, int l) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f4* s4 = reinterpret_cast<f4*>(s);
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i) s4[i * 64 + l] = f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
+    ldsOrder();
+#pragma unroll
+    for (int p = 0; p < D; p += 2) {  // row l: 16-byte reads (D even), lanes 16 D bytes apart
+      const f4 u = reinterpret_cast<const f4*>(s)[(l * D + p) / 2];
+      R.v[j][p] = f2{u.x, u.y};
+      R.v[j][p + 1] = f2{u.z, u.w};
+    }
+    ldsOrder();
+  }
+}
+
 // Load block b (rows b V .. b V + 511) and transpose to rows. Loads past the input's end read 0.
 template <int D>
 __device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kCf32>& R, f2* s, int l) {
@@ -369,20 +389,7 @@ __device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kCf32
       R.v[j][2 * i + 1] = f2{u.z, u.w};
     }
   }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    f4* s4 = reinterpret_cast<f4*>(s);
-#pragma unroll
-    for (int i = 0; i < D / 2; ++i) s4[i * 64 + l] = f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
-    ldsOrder();
-#pragma unroll
-    for (int p = 0; p < D; p += 2) {  // row l: 16-byte reads (D even), lanes 16 D bytes apart
-      const f4 u = reinterpret_cast<const f4*>(s)[(l * D + p) / 2];
-      R.v[j][p] = f2{u.x, u.y};
-      R.v[j][p + 1] = f2{u.z, u.w};
-    }
-    ldsOrder();
-  }
+  transposeRows<D>(R, s, l);
 }
 
 template <int D>
@@ -502,6 +509,52 @@ __device__ void directBlock(const Args& a, int64_t b, int l) {
   }
 }
 
+// The block's outputs from its rows: D forward FFTs (two phases at a time), Y = sum_p X_p G_p,
+// one inverse FFT, the first V outputs stored (AM envelope or complex).
+template <int D, int IN, int EPI>
+__device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& R, int64_t b, const Lds& L, int l) {
+  constexpr int NP = (D % 2 == 0) ? 2 : 1;  // phases transformed together
+  f2 acc[1][8];
+#pragma unroll
+  for (int d = 0; d < 8; ++d) acc[0][d] = f2{0.0f, 0.0f};
+#pragma unroll
+  for (int p = 0; p < D; p += NP) {
+    f2 z[NP][8];
+#pragma unroll
+    for (int n = 0; n < NP; ++n)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[n][j] = R.point(j, p + n);
+    fftFwd<NP>(z, L, l);
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+      f2 g[8], u[8];
+#pragma unroll
+      for (int d = 0; d < 8; d += 2) {
+        const f4 v = L.g[((p + n) * 4 + d / 2) * 64 + l];
+        g[d] = f2{v.x, v.y};
+        g[d + 1] = f2{v.z, v.w};
+      }
+#pragma unroll
+      for (int d = 0; d < 8; ++d) u[d] = cmac1(z[n][d], g[d], acc[0][d]);
+#pragma unroll
+      for (int d = 0; d < 8; ++d) acc[0][d] = cmul2(z[n][d], g[d], u[d]);
+    }
+  }
+  ifft512(acc, L, l);
+  const int64_t k0 = b * (int64_t)a.V;
+#pragma unroll
+  for (int h = 0; h < 8; ++h) {
+    const int m = l + 64 * h;
+    const int64_t k = k0 + m;
+    if (m < a.V && k < a.nOut) {
+      if (EPI == kAm)
+        reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc[0][h]);
+      else
+        reinterpret_cast<f2*>(a.out)[k] = acc[0][h];
+    }
+  }
+}
+
 template <int D, int IN, int EPI>
 __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) f2 lds[];
@@ -532,47 +585,50 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
       directBlock<D, IN, EPI>(a, b, l);
       continue;
     }
-    constexpr int NP = (D % 2 == 0) ? 2 : 1;  // phases transformed together
-    f2 acc[1][8];
-#pragma unroll
-    for (int d = 0; d < 8; ++d) acc[0][d] = f2{0.0f, 0.0f};
-#pragma unroll
-    for (int p = 0; p < D; p += NP) {
-      f2 z[NP][8];
-#pragma unroll
-      for (int n = 0; n < NP; ++n)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) z[n][j] = R.point(j, p + n);
-      fftFwd<NP>(z, L, l);
-#pragma unroll
-      for (int n = 0; n < NP; ++n) {
-        f2 g[8], u[8];
-#pragma unroll
-        for (int d = 0; d < 8; d += 2) {
-          const f4 v = L.g[((p + n) * 4 + d / 2) * 64 + l];
-          g[d] = f2{v.x, v.y};
-          g[d + 1] = f2{v.z, v.w};
-        }
-#pragma unroll
-        for (int d = 0; d < 8; ++d) u[d] = cmac1(z[n][d], g[d], acc[0][d]);
-#pragma unroll
-        for (int d = 0; d < 8; ++d) acc[0][d] = cmul2(z[n][d], g[d], u[d]);
-      }
-    }
-    ifft512(acc, L, l);
-    const int64_t k0 = b * (int64_t)a.V;
-#pragma unroll
-    for (int h = 0; h < 8; ++h) {
-      const int m = l + 64 * h;
-      const int64_t k = k0 + m;
-      if (m < a.V && k < a.nOut) {
-        if (EPI == kAm)
-          reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc[0][h]);
-        else
-          reinterpret_cast<f2*>(a.out)[k] = acc[0][h];
-      }
-    }
+    convolveBlock<D, IN, EPI>(a, R, b, L, l);
   }
+}
+
+// ---- one wave per SIMD with the next block's loads in flight (D = 1) ---------------------------
+// The 8-wave kernels overlap loads with FFT math only through their two waves per SIMD running out
+// of phase (the rows take 128-160 VGPRs). firFftD1PfKernel runs ONE wave per SIMD (the whole
+// 512-entry register file) and loads the next block (32 buffer_load_dwordx4 per lane, 128
+// registers) while the current block is transformed: the compiler places the in-flight block in
+// AGPRs (the half of the file VALU code does not otherwise use) and waits for it only when the
+// next iteration drains it into VGPRs. Measured (tools/exp/run_fft_variants.sh, one box): C4
+// 892 -> 850 us per 2^27 samples, bit-identical. The same scheme at D = 10 (C3) is SLOWER (543 ->
+// 640 us): one wave per SIMD exposes the LDS latency of the transposes and FFT exchanges, which
+// the 8-wave kernel hides behind its second wave, and the D = 10 block has 6x less FFT work per
+// loaded byte to hide the loads under.
+constexpr int kPfWaves = 4;
+
+template <int D>
+struct PrefetchCf {
+  f4 u[8][D / 2];  // 16-byte unit 64 i + l of row group j, in AGPRs
+};
+
+// Issue block b's loads (past the input's end, or past the last block, they read zeros).
+template <int D>
+__device__ __forceinline__ void issueBlockLoads(const Args& a, int64_t b, PrefetchCf<D>& P, int l) {
+  const int64_t off = b < a.nBlocks ? b * (int64_t)a.V * D * 8 : 0;
+  const auto rs = blockRsrc((const char*)a.in + off, b < a.nBlocks ? a.inBytes - off : 0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i)
+      P.u[j][i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((j * D / 2 + i) * 64 + l) * 16, 0, 0));
+}
+
+template <int D>
+__device__ __forceinline__ void drainBlockLoads(const PrefetchCf<D>& P, Rows<D, kCf32>& R) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < D / 2; ++i) {
+      const f4 u = P.u[j][i];
+      R.v[j][2 * i] = f2{u.x, u.y};
+      R.v[j][2 * i + 1] = f2{u.z, u.w};
+    }
 }
 
 // ---- D = 1: eight output phases per block from eight shared input-phase spectra -----------------
@@ -612,18 +668,9 @@ __device__ void directBlockD1(const Args& a, int64_t b, int l) {
   }
 }
 
-template <int EPI>
-__global__ void __launch_bounds__(kThreads) firFftD1Kernel(Args a) {
-  constexpr int D = 8;  // input phases (rows of 8 samples)
-  extern __shared__ __attribute__((aligned(16))) f2 lds[];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
-  f2* twAll = lds + D * 8 * 64;
-  f2* omegaAll = twAll + kTw + kWaves * scratchComplex<D>(kCf32);
-  Lds L;
-  L.g = reinterpret_cast<f4*>(lds);
-  L.tw = reinterpret_cast<const f4*>(twAll) + l;
-  L.scratch = twAll + kTw + w * scratchComplex<D>(kCf32);
-  for (int n = threadIdx.x; n < kOmega; n += kThreads) {
+// The w^k table (layout F, per-lane float4 pairs like G), filled by the workgroup's threads.
+__device__ __forceinline__ void fillOmega(f2* omegaAll, int threads) {
+  for (int n = threadIdx.x; n < kOmega; n += threads) {
     // complex n = ((d / 2) 64 + lane) 2 + (d & 1); layout F: lane = 8 k0 + c holds k0 + 8 c + 64 d
     const int lane = (n >> 1) & 63, d = 2 * (n >> 7) + (n & 1);
     const int k = (lane >> 3) + 8 * (lane & 7) + 64 * d;
@@ -631,81 +678,108 @@ __global__ void __launch_bounds__(kThreads) firFftD1Kernel(Args a) {
     sincospi(2.0 * k / kM, &sn, &cs);
     omegaAll[n] = f2{(float)cs, (float)sn};
   }
-  buildTables<D, kCf32>(a, twAll, L, w, l);  // (its barriers also publish the w^k table)
-  const f4* omega = reinterpret_cast<const f4*>(omegaAll) + l;
-  if (w >= kWaves / 2) {
-    for (int i = 0; i < GSDR_FFT_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
+// One D = 1 block: the eight input-phase spectra, then per output phase the spectral sum, one
+// inverse FFT and the stores.
+template <int EPI>
+__device__ __forceinline__ void convolveBlockD1(const Args& a, const Rows<8, kCf32>& R, int64_t b, const Lds& L,
+                                                const f4* omega, int l) {
+  constexpr int D = 8;
+  // the eight input-phase spectra, in place of the rows
+  f2 X[D][8];
+#pragma unroll
+  for (int p = 0; p < D; p += 2) {
+    f2 z[2][8];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[n][j] = R.point(j, p + n);
+    fftFwd<2>(z, L, l);
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int d = 0; d < 8; ++d) X[p + n][d] = z[n][d];
   }
-  const int64_t stride = (int64_t)gridDim.x * kWaves;
-  for (int64_t b = (int64_t)blockIdx.x * kWaves + w; b < a.nBlocks; b += stride) {
+  const int64_t row0 = b * (int64_t)a.V;
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    f2 acc[1][8], sh[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      acc[0][d] = f2{0.0f, 0.0f};
+      sh[d] = f2{0.0f, 0.0f};
+    }
+#pragma unroll
+    for (int p = 0; p < D; ++p) {
+      f2 g[8];
+#pragma unroll
+      for (int d = 0; d < 8; d += 2) {
+        const f4 v = L.g[(p * 4 + d / 2) * 64 + l];
+        g[d] = f2{v.x, v.y};
+        g[d + 1] = f2{v.z, v.w};
+      }
+      const int t = p + r;
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        if (t < D) acc[0][d] = cmac(X[t][d], g[d], acc[0][d]);
+        else sh[d] = cmac(X[t - D][d], g[d], sh[d]);
+      }
+    }
+    if (r > 0) {  // the one-row advance of the wrapped phases
+#pragma unroll
+      for (int d = 0; d < 8; d += 2) {
+        const f4 v = omega[(d / 2) * 64];
+        acc[0][d] = cmac(sh[d], f2{v.x, v.y}, acc[0][d]);
+        acc[0][d + 1] = cmac(sh[d + 1], f2{v.z, v.w}, acc[0][d + 1]);
+      }
+    }
+    ifft512(acc, L, l);
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      const int m = l + 64 * h;
+      const int64_t k = 8 * (row0 + m) + r;
+      if (m < a.V && k < a.nOut) {
+        if (EPI == kAm)
+          reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc[0][h]);
+        else
+          reinterpret_cast<f2*>(a.out)[k] = acc[0][h];
+      }
+    }
+  }
+}
+
+// D = 1 with one wave per SIMD and the next block's loads in flight into AGPRs (as firFftPfKernel).
+template <int EPI>
+__global__ void __launch_bounds__(kPfWaves * kWave) __attribute__((amdgpu_waves_per_eu(1, 1)))
+firFftD1PfKernel(Args a) {
+  constexpr int D = 8;
+  extern __shared__ __attribute__((aligned(16))) f2 lds[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  f2* twAll = lds + D * 8 * 64;
+  f2* omegaAll = twAll + kTw + kPfWaves * scratchComplex<D>(kCf32);
+  Lds L;
+  L.g = reinterpret_cast<f4*>(lds);
+  L.tw = reinterpret_cast<const f4*>(twAll) + l;
+  L.scratch = twAll + kTw + w * scratchComplex<D>(kCf32);
+  fillOmega(omegaAll, kPfWaves * kWave);
+  buildTables<D, kCf32, kPfWaves>(a, twAll, L, w, l);  // (its barriers also publish the w^k table)
+  const f4* omega = reinterpret_cast<const f4*>(omegaAll) + l;
+  const int64_t stride = (int64_t)gridDim.x * kPfWaves;
+  int64_t b = (int64_t)blockIdx.x * kPfWaves + w;
+  PrefetchCf<D> P;
+  issueBlockLoads<D>(a, b, P, l);
+  for (; b < a.nBlocks; b += stride) {
     Rows<D, kCf32> R;
-    loadRows<D>(a, b, R, L.scratch, l);
+    drainBlockLoads<D>(P, R);
+    issueBlockLoads<D>(a, b + stride, P, l);
+    transposeRows<D>(R, L.scratch, l);
     if (blockNeedsDirect<D, kCf32>(a, R, b, l)) {
       if (l == 0) atomicAdd(&gDirectBlocks, 1ull);
       directBlockD1<EPI>(a, b, l);
       continue;
     }
-    // the eight input-phase spectra, in place of the rows
-    f2 X[D][8];
-#pragma unroll
-    for (int p = 0; p < D; p += 2) {
-      f2 z[2][8];
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) z[n][j] = R.point(j, p + n);
-      fftFwd<2>(z, L, l);
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int d = 0; d < 8; ++d) X[p + n][d] = z[n][d];
-    }
-    const int64_t row0 = b * (int64_t)a.V;
-#pragma unroll
-    for (int r = 0; r < D; ++r) {
-      f2 acc[1][8], sh[8];
-#pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        acc[0][d] = f2{0.0f, 0.0f};
-        sh[d] = f2{0.0f, 0.0f};
-      }
-#pragma unroll
-      for (int p = 0; p < D; ++p) {
-        f2 g[8];
-#pragma unroll
-        for (int d = 0; d < 8; d += 2) {
-          const f4 v = L.g[(p * 4 + d / 2) * 64 + l];
-          g[d] = f2{v.x, v.y};
-          g[d + 1] = f2{v.z, v.w};
-        }
-        const int t = p + r;
-#pragma unroll
-        for (int d = 0; d < 8; ++d) {
-          if (t < D) acc[0][d] = cmac(X[t][d], g[d], acc[0][d]);
-          else sh[d] = cmac(X[t - D][d], g[d], sh[d]);
-        }
-      }
-      if (r > 0) {  // the one-row advance of the wrapped phases
-#pragma unroll
-        for (int d = 0; d < 8; d += 2) {
-          const f4 v = omega[(d / 2) * 64];
-          acc[0][d] = cmac(sh[d], f2{v.x, v.y}, acc[0][d]);
-          acc[0][d + 1] = cmac(sh[d + 1], f2{v.z, v.w}, acc[0][d + 1]);
-        }
-      }
-      ifft512(acc, L, l);
-#pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        const int m = l + 64 * h;
-        const int64_t k = 8 * (row0 + m) + r;
-        if (m < a.V && k < a.nOut) {
-          if (EPI == kAm)
-            reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc[0][h]);
-          else
-            reinterpret_cast<f2*>(a.out)[k] = acc[0][h];
-        }
-      }
-    }
+    convolveBlockD1<EPI>(a, R, b, L, omega, l);
   }
 }
 
@@ -744,8 +818,8 @@ hipError_t launchD(fftfir::Args a, hipStream_t stream) {
 template <int EPI>
 hipError_t launchD1(fftfir::Args a, hipStream_t stream) {
   using namespace fftfir;
-  auto kernel = firFftD1Kernel<EPI>;
-  const size_t lds = ldsBytes<8, kCf32>() + (size_t)kOmega * sizeof(f2);
+  auto kernel = firFftD1PfKernel<EPI>;
+  const size_t lds = (size_t)(8 * 8 * 64 + kTw + kPfWaves * scratchComplex<8>(kCf32) + kOmega) * sizeof(f2);
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -753,9 +827,9 @@ hipError_t launchD1(fftfir::Args a, hipStream_t stream) {
     attr = true;
   }
   const int64_t maxGroups = cuCount();
-  int64_t groups = (a.nBlocks + kWaves - 1) / kWaves;
+  int64_t groups = (a.nBlocks + kPfWaves - 1) / kPfWaves;
   if (groups > maxGroups) groups = maxGroups;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)groups), dim3(kThreads), lds, stream, a);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)groups), dim3(kPfWaves * kWave), lds, stream, a);
   return hipGetLastError();
 }
 
@@ -777,7 +851,7 @@ hipError_t launchFft(fftfir::Args a, size_t D, hipStream_t stream) {
 // at least 64 outputs per block, and the loads' alignment (cf32: 16-byte input; int8 IQ: 4-byte).
 bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int8Iq) {
   const size_t D = decimation < 1 ? 1 : decimation;
-  if (D == 1) {  // cf32: eight output phases per block (firFftD1Kernel), up to 3 584 taps
+  if (D == 1) {  // cf32: eight output phases per block (firFftD1PfKernel), up to 3 584 taps
     const size_t Q = (tapCount + 7) / 8;
     return !int8Iq && tapCount >= 256 && Q <= (size_t)fftfir::kM - 64 && ((uintptr_t)in & 15) == 0;
   }

@@ -12,5 +12,6 @@ TAILN=6 run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 200 
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench_default 400 python bench.py
 run bench_c2 200 python bench.py --workload c2 --steps 20 --warmup 3 --no-cpu-baseline
+run bench_c4 200 python bench.py --workload c4 --steps 20 --warmup 3 --no-cpu-baseline
 run bench_c5 200 python bench.py --workload c5 --steps 20 --warmup 3 --no-cpu-baseline
 echo "full validation done"
