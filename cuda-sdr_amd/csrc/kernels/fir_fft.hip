@@ -541,16 +541,20 @@ __device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& 
     }
   }
   ifft512(acc, L, l);
+  // outputs k0 + m, m < nv: the bound and the base are wave-uniform, so the lane math stays
+  // 32-bit (per-lane 64-bit output indices were spilled to scratch, and each reload between the
+  // stores waited for the stores before it: s_waitcnt vmcnt(0))
   const int64_t k0 = b * (int64_t)a.V;
+  const int64_t left = a.nOut - k0;
+  const int nv = __builtin_amdgcn_readfirstlane((int)(left < a.V ? left : a.V));
 #pragma unroll
   for (int h = 0; h < 8; ++h) {
     const int m = l + 64 * h;
-    const int64_t k = k0 + m;
-    if (m < a.V && k < a.nOut) {
+    if (m < nv) {
       if (EPI == kAm)
-        reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc[0][h]);
+        (reinterpret_cast<float*>(a.out) + k0)[m] = amEnvelope(acc[0][h]);
       else
-        reinterpret_cast<f2*>(a.out)[k] = acc[0][h];
+        (reinterpret_cast<f2*>(a.out) + k0)[m] = acc[0][h];
     }
   }
 }
@@ -735,15 +739,19 @@ __device__ __forceinline__ void convolveBlockD1(const Args& a, const Rows<8, kCf
       }
     }
     ifft512(acc, L, l);
+    // outputs 8 (row0 + m) + r for m < nv (wave-uniform bound and base, 32-bit lane math)
+    const int64_t left = a.nOut - 8 * row0 - r;
+    const int64_t rows = left <= 0 ? 0 : (left + 7) / 8;
+    const int nv = __builtin_amdgcn_readfirstlane((int)(rows < a.V ? rows : a.V));
+    const int64_t base = 8 * row0 + r;
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
       const int m = l + 64 * h;
-      const int64_t k = 8 * (row0 + m) + r;
-      if (m < a.V && k < a.nOut) {
+      if (m < nv) {
         if (EPI == kAm)
-          reinterpret_cast<float*>(a.out)[k] = amEnvelope(acc[0][h]);
+          (reinterpret_cast<float*>(a.out) + base)[8 * m] = amEnvelope(acc[0][h]);
         else
-          reinterpret_cast<f2*>(a.out)[k] = acc[0][h];
+          (reinterpret_cast<f2*>(a.out) + base)[8 * m] = acc[0][h];
       }
     }
   }
