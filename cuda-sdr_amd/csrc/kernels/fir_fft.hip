@@ -44,9 +44,6 @@
 #include <atomic>
 #include <cmath>
 
-#ifndef GSDR_FFT_STAGGER
-#define GSDR_FFT_STAGGER 1  // s_sleep(127) rounds before waves 4-7 start (~64 x 127 cycles each)
-#endif
 
 namespace gsdr_amd {
 namespace fftfir {
@@ -569,13 +566,6 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   L.tw = reinterpret_cast<const f4*>(twAll) + l;
   L.scratch = twAll + kTw + w * scratchComplex<D>(IN);
   buildTables<D, IN>(a, twAll, L, w, l);
-  if (w >= kWaves / 2) {
-    // stagger: the second-dispatched half of the waves (one per SIMD) starts ~4 us later, so the
-    // two waves of each SIMD run out of phase - one loading its block while the other computes -
-    // instead of all eight loading, then all computing (C3: 675 -> 591 us per launch,
-    // tools/exp/run_fft_variants.sh; larger delays resynchronise and do not help)
-    for (int i = 0; i < GSDR_FFT_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-  }
 
   // round r: workgroup g's wave w takes block (r * groups + g) * kWaves + w, so in every round
   // the grid streams one contiguous stretch of the input (DRAM-friendly, like a grid-stride copy)
@@ -589,7 +579,15 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
       directBlock<D, IN, EPI>(a, b, l);
       continue;
     }
+    // The two waves of a SIMD overlap one's loads with the other's FFTs only while they are out
+    // of phase. The wave in its FFT part runs at raised issue priority, so it is not slowed by
+    // the other wave's transposition and guard work: it finishes first and the pair settles into
+    // alternation - C3 513 -> 487 us per launch (tools/exp/run_fft_variants.sh, bit-identical).
+    // This replaces the start-up stagger (s_sleep for half the waves) of earlier builds, which
+    // is neutral on top of it.
+    __builtin_amdgcn_s_setprio(2);
     convolveBlock<D, IN, EPI>(a, R, b, L, l);
+    __builtin_amdgcn_s_setprio(0);
   }
 }
 
