@@ -20,13 +20,13 @@ VARIANT_DECLS
 
 typedef hipError_t (*LaunchFn)(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t);
 
-__global__ void fillKernel(float* x, size_t n, uint64_t seed) {
+__global__ void fillKernel(float* x, size_t n, uint64_t seed, float noise) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const double ph = 2.0 * M_PI * fmod(0.013 * (double)(i / 2), 1.0);
     uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z ^= z >> 31;
-    x[i] = (float)((i & 1) ? sin(ph) : cos(ph)) + 0.01f * ((float)(int32_t)(z >> 32) * (1.0f / 2147483648.0f));
+    x[i] = (float)((i & 1) ? sin(ph) : cos(ph)) + noise * ((float)(int32_t)(z >> 32) * (1.0f / 2147483648.0f));
   }
 }
 
@@ -205,7 +205,8 @@ int main() {
       for (size_t i = 0; i < inBytes; ++i) h[i] = (int8_t)(100.0 * cos(0.37 * (double)i) + (double)((i * 7919) % 7) - 3);
       hipMemcpy(x, h.data(), inBytes, hipMemcpyHostToDevice);
     } else {
-      fillKernel<<<1024, 256>>>((float*)x, 2 * nIn, 12345);
+      // FFT_BENCH_NOISE: amplitude of the uniform noise on the tone (default 0.01; ~1 is wideband)
+      fillKernel<<<1024, 256>>>((float*)x, 2 * nIn, 12345, getenv("FFT_BENCH_NOISE") ? (float)atof(getenv("FFT_BENCH_NOISE")) : 0.01f);
     }
     std::vector<float> ht(sh.T);
     for (size_t j = 0; j < sh.T; ++j) {
