@@ -17,9 +17,9 @@ notrans|-DGSDR_FFT_EXP=4
 noguard|-DGSDR_FFT_EXP=8
 nostore|-DGSDR_FFT_EXP=16
 fft_only|-DGSDR_FFT_EXP=30
-rowload|-DGSDR_FFT_EXP=32
-rowload_only|-DGSDR_FFT_EXP=57
-rowload_nofft|-DGSDR_FFT_EXP=33
+
+
+
 load_only|-DGSDR_FFT_EXP=29"}
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
