@@ -14,6 +14,8 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(PKG_DIR, "..", "lib", "libgpusdrpipeline.so"))
+# A/B builds of the library (tools/exp) may be named here; the in-tree build is the default.
+LIB_PATH = os.environ.get("GSDR_LIB") or LIB_PATH
 
 _lib = None
 
