@@ -1438,12 +1438,9 @@ template <int F16, int KS, int G, int EPI>
 hipError_t launchCfG(const CfFirArgs& a, size_t lds, int grid, hipStream_t stream) {
   auto kernel = F16 == 2 ? &firCfF16MfmaKernel<KS, G, EPI, true>
                          : (F16 == 1 ? &firCfF16MfmaKernel<KS, G, EPI, false> : &firCfMfmaKernel<KS, G, EPI>);
-  static std::once_flag once;
-  static hipError_t attrErr = hipSuccess;
-  std::call_once(once, [kernel] {
-    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+  // per launch (cheap; per device, no process-wide once-flag)
+  const hipError_t attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   kCfDynLdsMax);
-  });
   if (attrErr != hipSuccess) return attrErr;
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(kCfThreads), lds, stream, a);
   return hipGetLastError();
@@ -1483,12 +1480,9 @@ hipError_t launchCfAny(const CfFirArgs& a, size_t lds, int grid, int epi, hipStr
 
 template <int KS, int G, int EPI>
 hipError_t launchI8DecG(const I8DecArgs& a, size_t lds, int grid, hipStream_t stream) {
-  static std::once_flag once;
-  static hipError_t attrErr = hipSuccess;
-  std::call_once(once, [] {
-    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(&firI8DecMfmaKernel<KS, G, EPI>),
+  // per launch (cheap; per device, no process-wide once-flag)
+  const hipError_t attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(&firI8DecMfmaKernel<KS, G, EPI>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, kCfDynLdsMax);
-  });
   if (attrErr != hipSuccess) return attrErr;
   hipLaunchKernelGGL((firI8DecMfmaKernel<KS, G, EPI>), dim3(grid), dim3(kCfThreads), lds, stream, a);
   return hipGetLastError();
@@ -1497,12 +1491,9 @@ hipError_t launchI8DecG(const I8DecArgs& a, size_t lds, int grid, hipStream_t st
 template <int KS, int G, int EPI>
 hipError_t launchCfWsG(const CfFirArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
   auto kernel = &firCfWsKernel<KS, G, EPI>;
-  static std::once_flag once;
-  static hipError_t attrErr = hipSuccess;
-  std::call_once(once, [kernel] {
-    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+  // per launch (cheap; per device, no process-wide once-flag)
+  const hipError_t attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   kCfDynLdsMax);
-  });
   if (attrErr != hipSuccess) return attrErr;
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWsThreads), lds, stream, a, Wl);
   return hipGetLastError();
@@ -1537,12 +1528,9 @@ hipError_t launchCfWsAny(const CfFirArgs& a, int Wl, size_t lds, int grid, int e
 template <int KS, int G, int EPI>
 hipError_t launchI8WsG(const I8DecArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
   auto kernel = &firI8WsKernel<KS, G, EPI>;
-  static std::once_flag once;
-  static hipError_t attrErr = hipSuccess;
-  std::call_once(once, [kernel] {
-    attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+  // per launch (cheap; per device, no process-wide once-flag)
+  const hipError_t attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   kCfDynLdsMax);
-  });
   if (attrErr != hipSuccess) return attrErr;
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWsThreads), lds, stream, a, Wl);
   return hipGetLastError();
@@ -1630,15 +1618,51 @@ uint32_t takeWsAborts(int dev) {
   return h == nullptr ? 0u : __atomic_exchange_n(h, 0u, __ATOMIC_SEQ_CST);
 }
 
-// Before a wave-specialised launch: report an earlier launch's abort, and arm this one.
-hipError_t wsPrepare(int32_t& spinLimit, uint32_t*& abortOut) {
+// Completion marker of the last eager (not captured) wave-specialised launch per device.
+hipEvent_t gLastWs[kMaxDevices];
+
+// Before a wave-specialised launch: report an earlier launch's abort, and arm this one. The abort
+// word is read only once the device's last eager WS launch has completed (its event has fired:
+// after any synchronisation the caller makes, deterministically), never while that kernel may
+// still be writing it; an abort not yet settled is reported by a later call. Under stream capture
+// nothing is read (a graph executor checks after its replays, gsdrAmdWsTakeAborts).
+hipError_t wsPrepare(hipStream_t stream, int32_t& spinLimit, uint32_t*& abortOut) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  if (takeWsAborts(dev) != 0) return hipErrorLaunchTimeOut;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if ((e = hipStreamIsCapturing(stream, &cs)) != hipSuccess) return e;
+  if (cs == hipStreamCaptureStatusNone && dev >= 0 && dev < kMaxDevices) {
+    hipEvent_t ev;
+    {
+      std::lock_guard<std::mutex> lock(gAbortMu);
+      ev = gLastWs[dev];
+    }
+    const hipError_t q = ev == nullptr ? hipSuccess : hipEventQuery(ev);
+    if (q != hipSuccess && q != hipErrorNotReady) return q;
+    if (q == hipSuccess && takeWsAborts(dev) != 0) return hipErrorLaunchTimeOut;
+  }
   spinLimit = gWsSpinLimit.load(std::memory_order_relaxed);
   abortOut = wsAbortWord(dev);
   return hipSuccess;
+}
+
+// After an eager wave-specialised launch on `stream`: mark its completion for wsPrepare.
+hipError_t wsLaunched(hipStream_t stream, hipError_t launch) {
+  if (launch != hipSuccess) return launch;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess || dev < 0 || dev >= kMaxDevices) return e;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if ((e = hipStreamIsCapturing(stream, &cs)) != hipSuccess || cs != hipStreamCaptureStatusNone) return e;
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> lock(gAbortMu);
+    if (gLastWs[dev] == nullptr && (e = hipEventCreateWithFlags(&gLastWs[dev], hipEventDisableTiming)) != hipSuccess)
+      return e;
+    ev = gLastWs[dev];
+  }
+  return hipEventRecord(ev, stream);
 }
 
 }  // namespace
@@ -1697,8 +1721,8 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
       a.dbp = lds <= (size_t)kCfDynLdsMax;  // double-buffered partials when they fit
       if (!a.dbp) lds -= kCfPartialBytes;
       if (lds <= (size_t)kCfDynLdsMax) {
-        if (hipError_t e = wsPrepare(a.spinLimit, a.abortOut); e != hipSuccess) return e;
-        return launchCfWsAny(a, Wl, lds, grid, epi, stream);
+        if (hipError_t e = wsPrepare(stream, a.spinLimit, a.abortOut); e != hipSuccess) return e;
+        return wsLaunched(stream, launchCfWsAny(a, Wl, lds, grid, epi, stream));
       }
     }
   }
@@ -1783,8 +1807,8 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
       a.dbp = lds <= (size_t)kCfDynLdsMax;
       if (!a.dbp) lds -= kCfPartialBytes;
       if (lds <= (size_t)kCfDynLdsMax) {
-        if (hipError_t e = wsPrepare(a.spinLimit, a.abortOut); e != hipSuccess) return e;
-        return launchI8WsAny(a, Wl, lds, grid, epi, stream);
+        if (hipError_t e = wsPrepare(stream, a.spinLimit, a.abortOut); e != hipSuccess) return e;
+        return wsLaunched(stream, launchI8WsAny(a, Wl, lds, grid, epi, stream));
       }
     }
   }
@@ -1826,6 +1850,10 @@ void gsdrAmdSetWsSpinLimit(int32_t iterations) {
   gsdr_amd::gWsSpinLimit.store(iterations < 0 ? 0 : iterations, std::memory_order_relaxed);
 }
 int32_t gsdrAmdGetWsSpinLimit(void) { return gsdr_amd::gWsSpinLimit.load(std::memory_order_relaxed); }
+
+// Graph executors (am_chain, the stepping driver): aborts counted on `device` so far, cleared; no
+// synchronisation - call it once the replays of interest are known to have completed.
+uint32_t gsdrAmdWsTakeAborts(int32_t device) { return gsdr_amd::takeWsAborts(device); }
 
 hipError_t gsdrAmdWsAborts(int32_t device, uint64_t* count, int reset) {
   int prev = 0;

@@ -381,7 +381,13 @@ __device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kCf32
   for (int j = 0; j < 8; ++j) {
 #pragma unroll
     for (int i = 0; i < D / 2; ++i) {
-      const f4 u = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((j * D / 2 + i) * 64 + l) * 16, 0, 0));
+      // row groups 2-5 are read by this block only: non-temporal (aux 2), which saves fabric energy
+      // under the board power cap (C3 runs at 1400 W: time ~ energy); groups 0-1
+      // (the previous block's tail) and 6-7 (re-read by the next block) keep the default policy so
+      // the overlap stays an L2 hit. C3 490 -> 485 us, profiles/r03/exp/fft_nt_mid_ab.log
+      const int off = ((j * D / 2 + i) * 64 + l) * 16;
+      const f4 u = (j >= 2 && j <= 5) ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2))
+                                      : __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       R.v[j][2 * i] = f2{u.x, u.y};
       R.v[j][2 * i + 1] = f2{u.z, u.w};
     }
@@ -808,12 +814,9 @@ hipError_t launchD(fftfir::Args a, hipStream_t stream) {
   using namespace fftfir;
   auto kernel = firFftKernel<D, IN, EPI>;
   const size_t lds = ldsBytes<D, IN>();
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  // set per launch (cheap): a once-per-process flag would race between threads and miss other devices
+  const hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
   const int64_t maxGroups = cuCount();
   int64_t groups = (a.nBlocks + kWaves - 1) / kWaves;
   if (groups > maxGroups) groups = maxGroups;
@@ -826,12 +829,9 @@ hipError_t launchD1(fftfir::Args a, hipStream_t stream) {
   using namespace fftfir;
   auto kernel = firFftD1PfKernel<EPI>;
   const size_t lds = (size_t)(8 * 8 * 64 + kTw + kPfWaves * scratchComplex<8>(kCf32) + kOmega) * sizeof(f2);
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  // set per launch (cheap): a once-per-process flag would race between threads and miss other devices
+  const hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
   const int64_t maxGroups = cuCount();
   int64_t groups = (a.nBlocks + kPfWaves - 1) / kPfWaves;
   if (groups > maxGroups) groups = maxGroups;

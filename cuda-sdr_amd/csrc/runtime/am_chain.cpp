@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <initializer_list>
 #include <new>
 #include <vector>
 
@@ -69,15 +70,30 @@ struct gsdrAmChainImpl {
   float* resOut = nullptr;
   size_t resChunks = 0;
   bool resFirst = false;
-  // multi-chunk stepping (gsdrAmChainStepChunks): one cached graph of nChunks chunk steps over an
-  // AM window [ra history | nChunks La]
-  hipGraphExec_t multi = nullptr;
+  // multi-chunk stepping (gsdrAmChainStepChunks): cached graphs of nChunks chunk steps over an AM
+  // window [ra history | nChunks La], one per starting state (0 / 1 = the starting staging parity,
+  // 2 = the stream's first step): with an odd nChunks the parity flips every call, so one cached
+  // graph would be recaptured on every call
+  hipGraphExec_t multi[3] = {nullptr, nullptr, nullptr};
   float* amMulti = nullptr;
   size_t amMultiChunks = 0;
   const int8_t* multiIn = nullptr;
   float* multiOut = nullptr;
   size_t multiChunks = 0;
-  int multiKey = -1;  // 2 = starts with the first step, else the starting parity
+  size_t captures = 0;  // graphs instantiated (creation's three + every recapture; diagnostics)
+  hipEvent_t launched = nullptr;  // after the last step's launch: its completion settles WS aborts
+  bool launchedOnce = false;
+  // process-wide kernel settings baked into the cached graphs (kernel policy, FFT guard, WS spin
+  // limit) at their capture
+  uint64_t settings = 0;
+
+  static uint64_t currentSettings() {
+    const float g = gsdrAmdGetFftGuard();
+    uint32_t gb = 0;
+    std::memcpy(&gb, &g, sizeof gb);
+    return ((uint64_t)gsdrAmdGetKernelPolicy() * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)gb << 32) ^
+           (uint32_t)gsdrAmdGetWsSpinLimit();
+  }
   // pinned ring
   size_t slots = 0;
   int8_t* hostIn = nullptr;
@@ -94,7 +110,45 @@ struct gsdrAmChainImpl {
     if (e == hipSuccess) e = e2;
     if (e == hipSuccess) e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
     if (g != nullptr) (void)hipGraphDestroy(g);
+    if (e == hipSuccess) ++captures;
     return e;
+  }
+
+  // Step entry: fail if the previous step's launch completed with a WS abort; recapture the
+  // cached graphs when a process-wide kernel setting changed since their capture.
+  hipError_t enter() {
+    if (launchedOnce) {
+      const hipError_t q = hipEventQuery(launched);
+      if (q != hipSuccess && q != hipErrorNotReady) return q;
+      if (q == hipSuccess && gsdrAmdWsTakeAborts(device) != 0) return hipErrorLaunchTimeOut;
+    }
+    const uint64_t now = currentSettings();
+    if (now != settings) {
+      AMC_TRY(hipStreamSynchronize(stream));
+      for (hipGraphExec_t* g : {&first, &steady[0], &steady[1], &resident})
+        if (*g != nullptr) {
+          (void)hipGraphExecDestroy(*g);
+          *g = nullptr;
+        }
+      dropMulti();
+      settings = now;
+      AMC_TRY(capture(&first, true, 0));
+      AMC_TRY(capture(&steady[0], false, 0));
+      AMC_TRY(capture(&steady[1], false, 1));
+    }
+    return hipSuccess;
+  }
+  hipError_t markLaunched() {
+    launchedOnce = true;
+    return hipEventRecord(launched, stream);
+  }
+
+  void dropMulti() {
+    for (auto& m : multi)
+      if (m != nullptr) {
+        (void)hipGraphExecDestroy(m);
+        m = nullptr;
+      }
   }
 
   hipError_t enqueueCompute(bool firstStep, int p) {
@@ -170,6 +224,7 @@ struct gsdrAmChainImpl {
       if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : copyDone)
       if (ev) (void)hipEventDestroy(ev);
+    if (launched) (void)hipEventDestroy(launched);
     for (hipEvent_t ev : slotDone)
       if (ev) (void)hipEventDestroy(ev);
     (void)hipFree(taps);
@@ -179,7 +234,7 @@ struct gsdrAmChainImpl {
     (void)hipFree(am);
     (void)hipFree(amBig);
     if (resident) (void)hipGraphExecDestroy(resident);
-    if (multi) (void)hipGraphExecDestroy(multi);
+    dropMulti();
     (void)hipFree(amMulti);
     (void)hipFree(audio);
     if (hostIn) (void)hipHostFree(hostIn);
@@ -215,6 +270,8 @@ hipError_t build(gsdrAmChainImpl* c, const gsdrAmChainConfig& cfg) {
   AMC_TRY(hipMalloc(&c->audio, sizeof(float) * (c->na1 > c->naSteady ? c->na1 : c->naSteady)));
   for (auto& ev : c->readDone) AMC_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (auto& ev : c->copyDone) AMC_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  AMC_TRY(hipEventCreateWithFlags(&c->launched, hipEventDisableTiming));
+  c->settings = gsdrAmChainImpl::currentSettings();
   if (c->slots > 0) {
     AMC_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hostIn), 2 * c->L * c->slots, hipHostMallocDefault));
     AMC_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hostOut), sizeof(float) * c->naSteady * c->slots,
@@ -283,16 +340,20 @@ void gsdrAmChainDestroy(gsdrAmChain c) {
 
 hipStream_t gsdrAmChainStream(gsdrAmChain c) { return c == nullptr ? nullptr : c->stream; }
 
+size_t gsdrAmChainGraphCaptures(gsdrAmChain c) { return c == nullptr ? 0 : c->captures; }
+
 size_t gsdrAmChainNextOutputCount(gsdrAmChain c) { return c == nullptr ? 0 : c->nextOutputs(); }
 
 hipError_t gsdrAmChainStep(gsdrAmChain c, const int8_t* inputIq, float* output, size_t* outputCount) {
   if (c == nullptr || inputIq == nullptr || output == nullptr) return hipErrorInvalidValue;
   DevicePush push(c->device);
   AMC_TRY(push.err);
+  AMC_TRY(c->enter());
   const int p = c->steps == 0 ? 0 : (int)(c->steps & 1);
   const size_t n = c->nextOutputs();
   AMC_TRY(hipMemcpyAsync(c->staging[p] + 2 * c->r, inputIq, 2 * c->L, hipMemcpyDeviceToDevice, c->stream));
   AMC_TRY(hipGraphLaunch(c->graphFor(p), c->stream));
+  AMC_TRY(c->markLaunched());
   AMC_TRY(hipEventRecord(c->readDone[p], c->stream));
   AMC_TRY(hipMemcpyAsync(output, c->audio, sizeof(float) * n, hipMemcpyDeviceToDevice, c->stream));
   ++c->steps;
@@ -310,39 +371,39 @@ hipError_t gsdrAmChainStepChunks(gsdrAmChain c, const int8_t* inputIq, size_t nC
   if (c == nullptr || inputIq == nullptr || output == nullptr || nChunks == 0) return hipErrorInvalidValue;
   DevicePush push(c->device);
   AMC_TRY(push.err);
+  AMC_TRY(c->enter());
   const size_t n = gsdrAmChainChunksOutputCount(c, nChunks);
   const int key = c->steps == 0 ? 2 : (int)(c->steps & 1);
   if (nChunks > c->amMultiChunks) {  // grow the AM window (outside any capture)
     AMC_TRY(hipStreamSynchronize(c->stream));
-    if (c->multi != nullptr) (void)hipGraphExecDestroy(c->multi);
-    c->multi = nullptr;
+    c->dropMulti();
     (void)hipFree(c->amMulti);
     c->amMulti = nullptr;
     c->amMultiChunks = 0;
     AMC_TRY(hipMalloc(&c->amMulti, sizeof(float) * (c->ra + nChunks * c->La)));
     c->amMultiChunks = nChunks;
   }
-  if (c->multi == nullptr || c->multiIn != inputIq || c->multiOut != output || c->multiChunks != nChunks ||
-      c->multiKey != key) {
-    if (c->multi != nullptr) {
-      AMC_TRY(hipStreamSynchronize(c->stream));
-      AMC_TRY(hipGraphExecDestroy(c->multi));
-      c->multi = nullptr;
-    }
+  if (c->multiIn != inputIq || c->multiOut != output || c->multiChunks != nChunks) {
+    // new buffers or chunk count: every cached start state is stale
+    AMC_TRY(hipStreamSynchronize(c->stream));
+    c->dropMulti();
+    c->multiIn = inputIq;
+    c->multiOut = output;
+    c->multiChunks = nChunks;
+  }
+  if (c->multi[key] == nullptr) {
     hipGraph_t g = nullptr;
     AMC_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     hipError_t e = c->enqueueChunks(inputIq, nChunks, output, c->steps);
     const hipError_t e2 = hipStreamEndCapture(c->stream, &g);
     if (e == hipSuccess) e = e2;
-    if (e == hipSuccess) e = hipGraphInstantiate(&c->multi, g, nullptr, nullptr, 0);
+    if (e == hipSuccess) e = hipGraphInstantiate(&c->multi[key], g, nullptr, nullptr, 0);
     if (g != nullptr) (void)hipGraphDestroy(g);
     AMC_TRY(e);
-    c->multiIn = inputIq;
-    c->multiOut = output;
-    c->multiChunks = nChunks;
-    c->multiKey = key;
+    ++c->captures;
   }
-  AMC_TRY(hipGraphLaunch(c->multi, c->stream));
+  AMC_TRY(hipGraphLaunch(c->multi[key], c->stream));
+  AMC_TRY(c->markLaunched());
   // both staging parities were last read by this launch
   AMC_TRY(hipEventRecord(c->readDone[0], c->stream));
   AMC_TRY(hipEventRecord(c->readDone[1], c->stream));
@@ -363,6 +424,7 @@ hipError_t gsdrAmChainStepHost(gsdrAmChain c, size_t slot, size_t* outputCount) 
   if (c == nullptr || slot >= c->slots) return hipErrorInvalidValue;
   DevicePush push(c->device);
   AMC_TRY(push.err);
+  AMC_TRY(c->enter());
   const int p = c->steps == 0 ? 0 : (int)(c->steps & 1);
   const size_t n = c->nextOutputs();
   // the H2D copy may start once the step that last read staging[p] is done with it
@@ -372,6 +434,7 @@ hipError_t gsdrAmChainStepHost(gsdrAmChain c, size_t slot, size_t* outputCount) 
   AMC_TRY(hipEventRecord(c->copyDone[p], c->copyStream));
   AMC_TRY(hipStreamWaitEvent(c->stream, c->copyDone[p], 0));
   AMC_TRY(hipGraphLaunch(c->graphFor(p), c->stream));
+  AMC_TRY(c->markLaunched());
   AMC_TRY(hipEventRecord(c->readDone[p], c->stream));
   AMC_TRY(hipMemcpyAsync(c->hostOut + c->naSteady * slot, c->audio, sizeof(float) * n, hipMemcpyDeviceToHost,
                          c->stream));
@@ -395,6 +458,7 @@ hipError_t gsdrAmChainStepResident(gsdrAmChain c, const int8_t* inputIq, size_t 
   if (c == nullptr || inputIq == nullptr || output == nullptr || nChunks == 0) return hipErrorInvalidValue;
   DevicePush push(c->device);
   AMC_TRY(push.err);
+  AMC_TRY(c->enter());
   if (nChunks > c->amBigChunks) {  // grow the AM window (outside any capture)
     AMC_TRY(hipStreamSynchronize(c->stream));
     (void)hipFree(c->amBig);
@@ -418,6 +482,7 @@ hipError_t gsdrAmChainStepResident(gsdrAmChain c, const int8_t* inputIq, size_t 
     if (e == hipSuccess) e = hipGraphInstantiate(&c->resident, g, nullptr, nullptr, 0);
     if (g != nullptr) (void)hipGraphDestroy(g);
     AMC_TRY(e);
+    ++c->captures;
     c->resIn = inputIq;
     c->resOut = output;
     c->resChunks = nChunks;
@@ -425,6 +490,7 @@ hipError_t gsdrAmChainStepResident(gsdrAmChain c, const int8_t* inputIq, size_t 
   }
   const size_t n = c->residentAudio(nChunks);
   AMC_TRY(hipGraphLaunch(c->resident, c->stream));
+  AMC_TRY(c->markLaunched());
   // the AM history now sits at the front of amBig; the per-chunk window `am` is stale, so a later
   // per-chunk step would need a reset (documented in gsdr_amd.h)
   c->steps += nChunks;

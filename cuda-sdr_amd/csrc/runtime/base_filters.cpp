@@ -116,6 +116,19 @@ void BaseSink::foldWindowState(uint64_t& h) const noexcept {
   }
 }
 
+IRelocatableResizableBuffer* BaseSink::inputWindow(size_t port) const noexcept {
+  return port < mInputPorts.size() ? const_cast<IRelocatableResizableBuffer*>(mInputPorts[port].inputBuffer.get())
+                                   : nullptr;
+}
+
+bool BaseSink::inputWindowCheckedOut(size_t port) const noexcept {
+  return port < mInputPorts.size() && mInputPorts[port].bufferCheckedOut;
+}
+
+void BaseSink::setInputWindowCheckedOut(size_t port, bool checkedOut) noexcept {
+  if (port < mInputPorts.size()) mInputPorts[port].bufferCheckedOut = checkedOut;
+}
+
 BaseSource::BaseSource(std::vector<ImmutableRef<IBufferCopier>>&& outputPortBufferCopiers) noexcept
     : mOutputPortBufferCopiers(std::move(outputPortBufferCopiers)) {}
 

@@ -192,6 +192,28 @@ class RelocatableResizableBuffer final : public IRelocatableResizableBuffer {
   Status resize(size_t newSize) noexcept final;
   Status relocate(size_t dstOffset, size_t srcOffset, size_t length) noexcept final;
 
+  // Graph replay (SteppingDriver::doFilterGraphed): the window's whole host state - which
+  // allocation is live, which is the spare, the used range and the capacity - saved after a
+  // captured step and reinstated when that step is replayed. Holding the allocations also keeps
+  // the addresses the captured graph uses alive.
+  struct Snapshot {
+    Ref<IMemory> data, spare;
+    size_t offset = 0, end = 0, capacity = 0;
+  };
+  void save(Snapshot& s) const noexcept {
+    s.data = mData;
+    s.spare = mSpare;
+    s.offset = mRange->offset();
+    s.end = mRange->endOffset();
+    s.capacity = mRange->capacity();
+  }
+  Status restore(const Snapshot& s) noexcept {
+    mData = s.data;
+    mSpare = s.spare;
+    mRange->setCapacity(s.capacity);
+    return mRange->setUsedRange(s.offset, s.end);
+  }
+
  private:
   RelocatableResizableBuffer(IAllocator* allocator, const IBufferCopier* copier, IBufferRangeMutableCapacity* range)
       : mAllocator(allocator), mCopier(copier), mRange(range) {}

@@ -298,21 +298,29 @@ Status SteppingDriver::doSourceOutput(Source* source) {
 // ---- graph stepping -----------------------------------------------------------------------------
 // The steady state of a chain fed fixed-size chunks repeats: every node's window sits at one of a
 // few placements (lazy compaction cycles through them), and a step from a given placement enqueues
-// the same launches with the same arguments. So the step's device work is captured once per
-// placement and replayed. The host bookkeeping (window offsets, consume, commit) must still
-// advance, so a replayed step runs doFilter() under a stream capture that is thrown away - the
-// host logic runs, its launches are recorded instead of executed - and then launches the cached
-// executable graph: one launch instead of one per kernel / copy. A placement is captured only
-// the second time it is seen (the first time may still grow windows: allocation, no replay), and
-// the driver falls back to plain steps for good when a chain's state does not repeat (a tone
-// source's phase) or a node is not on `stream`.
+// the same launches with the same arguments and leaves the same host state behind. So the step is
+// captured once per placement - its device work as a hipGraph, its host outcome as every node's
+// window state (which allocation is live, used range, checkout flags) - and a replay reinstates
+// that host state and launches the graph: no per-node host logic, no per-kernel launches. A
+// placement is captured only the second time it is seen (the first time may still grow windows:
+// allocation, no replay), and the driver falls back to plain steps for good when a chain's state
+// does not repeat (a tone source's phase) or a node is not on `stream`.
 
 SteppingDriver::~SteppingDriver() {
   for (const CachedGraph& g : mGraphs) (void)hipGraphExecDestroy(g.exec);
+  if (mGraphDone != nullptr) (void)hipEventDestroy(mGraphDone);
 }
 
-bool SteppingDriver::chainState(hipStream_t stream, uint64_t& key) const noexcept {
+bool SteppingDriver::chainState(hipStream_t stream, uint64_t& key, std::vector<IGraphStepState*>* nodesOut) const
+    noexcept {
+  // process-wide kernel settings that become captured launch arguments: a replay must not run with
+  // values that changed since its capture (kernel policy, FFT guard ratio, WS spin limit)
+  const float guard = gsdrAmdGetFftGuard();
+  uint32_t guardBits = 0;
+  std::memcpy(&guardBits, &guard, sizeof guardBits);
   uint64_t h = 0xCBF29CE484222325ull ^ (uint64_t)gsdrAmdGetKernelPolicy();
+  h = (h ^ guardBits) * 0x100000001B3ull;
+  h = (h ^ (uint32_t)gsdrAmdGetWsSpinLimit()) * 0x100000001B3ull;
   // every connected node (a fixed order: by address)
   std::vector<Node*> nodes;
   for (Source* so : mSourceOrder) nodes.push_back(so);
@@ -320,10 +328,12 @@ bool SteppingDriver::chainState(hipStream_t stream, uint64_t& key) const noexcep
   std::sort(nodes.begin(), nodes.end());
   nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
   if (nodes.empty()) return false;
+  if (nodesOut != nullptr) nodesOut->clear();
   for (Node* n : nodes) {
-    const auto* g = dynamic_cast<const IGraphStepState*>(n);
+    auto* g = dynamic_cast<IGraphStepState*>(n);
     if (g == nullptr || g->graphStream() != stream || !g->graphState(h)) return false;
     h = (h ^ reinterpret_cast<uintptr_t>(n)) * 0x100000001B3ull;
+    if (nodesOut != nullptr) nodesOut->push_back(g);
   }
   key = h;
   return true;
@@ -343,19 +353,37 @@ Status SteppingDriver::captureStep(hipStream_t stream, hipGraph_t* graphOut) noe
   return Status_Success;
 }
 
+Status SteppingDriver::launchGraph(hipGraphExec_t exec, hipStream_t stream) noexcept {
+  SAFE_HIP_OR_RET_STATUS(hipGraphLaunch(exec, stream));
+  if (mGraphDone == nullptr) SAFE_HIP_OR_RET_STATUS(hipEventCreateWithFlags(&mGraphDone, hipEventDisableTiming));
+  SAFE_HIP_OR_RET_STATUS(hipEventRecord(mGraphDone, stream));
+  mGraphLaunched = true;
+  return Status_Success;
+}
+
 Status SteppingDriver::doFilterGraphed(hipStream_t stream) noexcept {
   try {
+    // a wave-specialised kernel inside an earlier replay that gave up a hand-off wait: reported
+    // once that replay has completed (the eager entry points cannot see graph launches)
+    if (mGraphLaunched) {
+      const hipError_t q = hipEventQuery(mGraphDone);
+      if (q != hipSuccess && q != hipErrorNotReady) SAFE_HIP_OR_RET_STATUS(q);
+      int dev = 0;
+      if (q == hipSuccess && hipStreamGetDevice(stream, &dev) == hipSuccess && gsdrAmdWsTakeAborts(dev) != 0) {
+        gsloge("SteppingDriver: a wave-specialised kernel in a replayed step aborted (hand-off wait timed out)");
+        return Status_RuntimeError;
+      }
+    }
     uint64_t key = 0;
-    if (mGraphOff || stream == nullptr || !chainState(stream, key)) {
+    std::vector<IGraphStepState*> nodes;
+    if (mGraphOff || stream == nullptr || !chainState(stream, key, &nodes)) {
       ++mStats.eager;
       return doFilter();
     }
     for (const CachedGraph& g : mGraphs) {
       if (g.key != key) continue;
-      hipGraph_t scratch = nullptr;  // host bookkeeping only; the recorded launches are discarded
-      FWD_IF_ERR(captureStep(stream, &scratch));
-      if (scratch != nullptr) (void)hipGraphDestroy(scratch);
-      SAFE_HIP_OR_RET_STATUS(hipGraphLaunch(g.exec, stream));
+      for (const auto& [node, state] : g.post) FWD_IF_ERR(node->restoreStepState(state));
+      FWD_IF_ERR(launchGraph(g.exec, stream));
       ++mStats.replayed;
       mGraphMisses = 0;
       return Status_Success;
@@ -381,8 +409,21 @@ Status SteppingDriver::doFilterGraphed(hipStream_t stream) noexcept {
     const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     SAFE_HIP_OR_RET_STATUS(ie);
-    mGraphs.push_back(CachedGraph{key, exec});
-    SAFE_HIP_OR_RET_STATUS(hipGraphLaunch(exec, stream));
+    CachedGraph cg{key, exec, {}};
+    bool saved = true;
+    cg.post.reserve(nodes.size());
+    for (IGraphStepState* n : nodes) {
+      cg.post.emplace_back(n, GraphNodeState{});
+      saved = saved && n->saveStepState(cg.post.back().second);
+    }
+    const Status ls = launchGraph(exec, stream);
+    if (saved && ls == Status_Success) {
+      mGraphs.push_back(std::move(cg));
+    } else {
+      if (ls == Status_Success) SAFE_HIP_OR_RET_STATUS(hipStreamSynchronize(stream));
+      (void)hipGraphExecDestroy(exec);
+    }
+    FWD_IF_ERR(ls);
     ++mStats.captured;
     return Status_Success;
   }

@@ -11,10 +11,13 @@
 //  * a cycle in the graph ends the step with Status_InvalidState instead of recursing forever.
 //
 // MI355X extension: doFilterGraphed(stream) - the same step, with its device work replayed from a
-// captured hipGraph once the chain's host state repeats (see driver.cpp).
+// captured hipGraph once the chain's host state repeats, and its host work replaced by reinstating
+// the host state the captured step left behind (see driver.cpp).
 #pragma once
 
 #include <gpusdrpipeline/Factories.h>
+
+#include "graph_state.h"
 
 #include <hip/hip_runtime_api.h>
 
@@ -101,14 +104,20 @@ class SteppingDriver final : public ISteppingDriver {
   struct CachedGraph {
     uint64_t key;
     hipGraphExec_t exec;
+    // every node's host state after the captured step, reinstated on replay instead of running
+    // the step's host logic again
+    std::vector<std::pair<IGraphStepState*, GraphNodeState>> post;
   };
   std::vector<CachedGraph> mGraphs;
   std::vector<uint64_t> mSeen;
   size_t mGraphMisses = 0;
   bool mGraphOff = false;
   GraphStats mStats;
-  bool chainState(hipStream_t stream, uint64_t& key) const noexcept;
+  hipEvent_t mGraphDone = nullptr;  // after the last graph launch: wave-specialised aborts settle
+  bool mGraphLaunched = false;
+  bool chainState(hipStream_t stream, uint64_t& key, std::vector<IGraphStepState*>* nodesOut) const noexcept;
   Status captureStep(hipStream_t stream, hipGraph_t* graphOut) noexcept;
+  Status launchGraph(hipGraphExec_t exec, hipStream_t stream) noexcept;
 
   ~SteppingDriver() final;
   REF_COUNTED_NO_DESTRUCTOR(SteppingDriver);

@@ -505,8 +505,10 @@ Status HostEgressSink::deliver(size_t keepInFlight) noexcept {
   const size_t ready = used > keepInFlight ? used - keepInFlight : 0;
   if (ready == 0) return Status_Success;
   try {
-    if (mReadPos != 0 && mReadPos == mFifo.size()) {
-      mFifo.clear();
+    // drop the consumed prefix once it is at least half the FIFO: a reader whose frame size does not
+    // line up with the step size never empties it, and the FIFO must not grow with the stream
+    if (mReadPos != 0 && 2 * mReadPos >= mFifo.size()) {
+      mFifo.erase(mFifo.begin(), mFifo.begin() + (ptrdiff_t)mReadPos);
       mReadPos = 0;
     }
     const uint8_t* src = in->readPtr();

@@ -27,6 +27,8 @@ class Fir final : public BaseFilter, public IGraphStepState {
     h = (h ^ reinterpret_cast<uintptr_t>(mTaps.get() ? mTaps->data() : nullptr)) * 0x100000001B3ull + mTapCount;
     return true;
   }
+  bool saveStepState(GraphNodeState& out) const noexcept final { return saveSinkWindows(*this, out); }
+  Status restoreStepState(const GraphNodeState& in) noexcept final { return restoreSinkWindows(*this, in); }
   static Result<Filter> create(SampleType tapType, SampleType elementType, size_t decimation, const float* taps,
                                size_t tapCount, ICudaCommandQueue* queue, IFactories* factories) noexcept;
 
@@ -67,6 +69,8 @@ class QuadAmDemod final : public BaseFilter, public IGraphStepState {
     foldWindowState(h);
     return true;
   }
+  bool saveStepState(GraphNodeState& out) const noexcept final { return saveSinkWindows(*this, out); }
+  Status restoreStepState(const GraphNodeState& in) noexcept final { return restoreSinkWindows(*this, in); }
   static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
@@ -89,6 +93,8 @@ class MultiplyCcc final : public BaseFilter, public IGraphStepState {
     foldWindowState(h);
     return true;
   }
+  bool saveStepState(GraphNodeState& out) const noexcept final { return saveSinkWindows(*this, out); }
+  Status restoreStepState(const GraphNodeState& in) noexcept final { return restoreSinkWindows(*this, in); }
   static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
@@ -112,6 +118,8 @@ class QuadFmDemod final : public BaseFilter, public IGraphStepState {
     foldWindowState(h);
     return true;
   }
+  bool saveStepState(GraphNodeState& out) const noexcept final { return saveSinkWindows(*this, out); }
+  Status restoreStepState(const GraphNodeState& in) noexcept final { return restoreSinkWindows(*this, in); }
   static Result<Filter> create(float gain, ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
@@ -134,6 +142,8 @@ class Int8ToFloat final : public BaseFilter, public IGraphStepState {
     foldWindowState(h);
     return true;
   }
+  bool saveStepState(GraphNodeState& out) const noexcept final { return saveSinkWindows(*this, out); }
+  Status restoreStepState(const GraphNodeState& in) noexcept final { return restoreSinkWindows(*this, in); }
   static Result<Filter> create(ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
@@ -152,6 +162,8 @@ class CosineSource final : public BaseSource, public IGraphStepState {
  public:
   hipStream_t graphStream() const noexcept final { return mQueue->cudaStream(); }
   bool graphState(uint64_t&) const noexcept final { return false; }  // the phase argument advances
+  bool saveStepState(GraphNodeState&) const noexcept final { return false; }
+  Status restoreStepState(const GraphNodeState&) noexcept final { return Status_InvalidState; }
 
   static Result<Source> create(bool complexOutput, float sampleRate, float frequency, ICudaCommandQueue* queue,
                                IFactories* factories) noexcept;
@@ -176,6 +188,8 @@ class HipMemcpyFilter final : public BaseFilter, public IGraphStepState {
     foldWindowState(h);
     return true;
   }
+  bool saveStepState(GraphNodeState& out) const noexcept final { return saveSinkWindows(*this, out); }
+  Status restoreStepState(const GraphNodeState& in) noexcept final { return restoreSinkWindows(*this, in); }
   static Result<Filter> create(hipMemcpyKind kind, ICudaCommandQueue* queue, IFactories* factories) noexcept;
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;

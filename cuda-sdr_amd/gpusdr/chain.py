@@ -40,7 +40,8 @@ def _L():
                 ("gsdrAmChainResidentOutputCount", [vp, sz], sz),
                 ("gsdrAmChainStepResident", [vp, vp, sz, vp, psz], err),
                 ("gsdrAmChainChunksOutputCount", [vp, sz], sz),
-                ("gsdrAmChainStepChunks", [vp, vp, sz, vp, psz], err)):
+                ("gsdrAmChainStepChunks", [vp, vp, sz, vp, psz], err),
+                ("gsdrAmChainGraphCaptures", [vp], sz)):
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
@@ -117,9 +118,10 @@ class AmChain:
         return _L().gsdrAmChainChunksOutputCount(self._h, n_chunks)
 
     def step_chunks(self, iq: torch.Tensor, n_chunks: int, out: torch.Tensor) -> int:
-        """n_chunks live-stream chunk steps (each copied through the staging window exactly as
-        step() does) as ONE cached graph launch; the audio of all of them lands contiguously in
-        out. Returns the audio count."""
+        """n_chunks live-stream chunk steps as ONE cached graph launch, output identical to n_chunks
+        step() calls; the audio of all of them lands contiguously in out. Chunks 1.. are read in
+        place, so iq must stay unmodified until the chain stream has run the launch. Returns the
+        audio count."""
         if iq.dtype != torch.int8 or not iq.is_cuda or iq.numel() < 2 * self.chunk * n_chunks:
             raise ValueError("iq must be a device int8 tensor of n_chunks chunks")
         n = self.chunks_output_count(n_chunks)
@@ -151,3 +153,7 @@ class AmChain:
 
     def reset(self):
         check(_L().gsdrAmChainReset(self._h), "gsdrAmChainReset")
+
+    def graph_captures(self) -> int:
+        """Graphs instantiated so far (3 at creation + every StepChunks / StepResident capture)."""
+        return _L().gsdrAmChainGraphCaptures(self._h)

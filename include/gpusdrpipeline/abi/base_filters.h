@@ -46,6 +46,14 @@ class GS_PUBLIC BaseSink : public virtual Sink {
    * address, used range, capacity, checkout flag) into h. Non-virtual: no vtable change. */
   void foldWindowState(uint64_t& h) const noexcept;
 
+ public:
+  /* MI355X extension (graph replay, driver.h): the input windows and their checkout flags, so the
+   * host state a captured step leaves behind can be saved and reinstated on replay. */
+  [[nodiscard]] size_t inputWindowCount() const noexcept { return mInputPorts.size(); }
+  [[nodiscard]] IRelocatableResizableBuffer* inputWindow(size_t port) const noexcept;
+  [[nodiscard]] bool inputWindowCheckedOut(size_t port) const noexcept;
+  void setInputWindowCheckedOut(size_t port, bool checkedOut) noexcept;
+
  private:
   const size_t mInputPortCount;
   ConstRef<IBufferSliceFactory> mSlicedBufferFactory;

@@ -132,9 +132,10 @@ GSDR_API void gsdrAmdSetKernelPolicy(uint32_t flags);
  * "fft", "i8-mfma", "i8-dec-mfma", "cf-mfma" or "valu" (diagnostics / benchmark labels). */
 GSDR_API const char* gsdrAmdFirKernelClass(int int8Iq, size_t tapCount, size_t decimation, const void* input);
 GSDR_API uint32_t gsdrAmdGetKernelPolicy(void);
-/* FFT FIR accuracy guard: a block whose loudest row (D consecutive samples, sum of max(|re|,|im|))
- * exceeds `ratio` times its quietest, or that holds inf/NaN, is computed in the direct fp32 form.
- * Default 8; 0 forces the direct form everywhere (tests). */
+/* FFT FIR accuracy guard: each FFT block is cut into segments of >= 16 consecutive samples; a block
+ * whose loudest segment's level (root of its energy sum |x|^2) exceeds `ratio` times its quietest
+ * segment's (compared on energies: hi <= ratio^2 lo), or that holds inf/NaN, is computed in the
+ * direct fp32 form. Default 8; 0 forces the direct form everywhere (tests). */
 GSDR_API void gsdrAmdSetFftGuard(float ratio);
 GSDR_API float gsdrAmdGetFftGuard(void);
 /* Diagnostics: blocks the FFT FIR computed in the direct form on `device` since the last reset
@@ -149,6 +150,11 @@ GSDR_API hipError_t gsdrAmdFftDirectBlocks(int32_t device, uint64_t* count, int 
 GSDR_API void gsdrAmdSetWsSpinLimit(int32_t iterations);
 GSDR_API int32_t gsdrAmdGetWsSpinLimit(void);
 GSDR_API hipError_t gsdrAmdWsAborts(int32_t device, uint64_t* count, int reset);
+/* The same count, read and cleared WITHOUT synchronising: for graph executors, which call it once
+ * the replays they launched are known to have completed (an event they recorded has fired). The
+ * eager entry points read it only after the device's last eager WS launch has completed, so which
+ * call reports an abort depends only on the caller's synchronisation, not on timing. */
+GSDR_API uint32_t gsdrAmdWsTakeAborts(int32_t device);
 
 GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
                                     uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,
@@ -196,10 +202,14 @@ GSDR_API size_t gsdrAmChainNextOutputCount(gsdrAmChain chain);
 /* One step from device memory: chunkSamples IQ pairs at inputIq (copied into the staging window),
  * audio written to `output` (device, gsdrAmChainNextOutputCount floats). Asynchronous. */
 GSDR_API hipError_t gsdrAmChainStep(gsdrAmChain chain, const int8_t* inputIq, float* output, size_t* outputCount);
-/* nChunks consecutive chunk steps in ONE launch: the chunks are contiguous at inputIq (device),
- * each is copied into the staging window and stepped exactly as gsdrAmChainStep does, and the audio
- * of all of them is written contiguously at `output` (gsdrAmChainChunksOutputCount floats). The
- * whole sequence is one graph, cached for the last (inputIq, nChunks, output, step parity). */
+/* nChunks consecutive chunk steps in ONE launch: the chunks are contiguous at inputIq (device), and
+ * the audio of all of them is written contiguously at `output` (gsdrAmChainChunksOutputCount
+ * floats), exactly as nChunks gsdrAmChainStep calls would produce. Chunk 0 is copied into the
+ * staging window behind the carried history; chunks 1.. are read IN PLACE (their RF history is the
+ * previous chunk's tail), so the input must stay valid and unmodified until the launch completes
+ * (e.g. until the chain stream is synchronised). The whole sequence is one graph; graphs are cached
+ * for the last (inputIq, nChunks, output), one per starting state (either staging parity, or the
+ * stream's first step), so an odd nChunks does not recapture on every call. */
 GSDR_API size_t gsdrAmChainChunksOutputCount(gsdrAmChain chain, size_t nChunks);
 GSDR_API hipError_t gsdrAmChainStepChunks(gsdrAmChain chain, const int8_t* inputIq, size_t nChunks, float* output,
                                           size_t* outputCount);
@@ -220,6 +230,13 @@ GSDR_API hipError_t gsdrAmChainWaitSlot(gsdrAmChain chain, size_t slot);
 GSDR_API size_t gsdrAmChainResidentOutputCount(gsdrAmChain chain, size_t nChunks);
 GSDR_API hipError_t gsdrAmChainStepResident(gsdrAmChain chain, const int8_t* inputIq, size_t nChunks, float* output,
                                             size_t* outputCount);
+/* Every step entry first checks the previous step's launch: once it has completed, a
+ * wave-specialised abort counted on the device (gsdrAmdWsTakeAborts) fails the call with
+ * hipErrorLaunchTimeOut. Cached graphs bake in the kernel policy, the FFT guard ratio and the WS
+ * spin limit of their capture; a step after any of them changed recaptures. */
+/* Graphs the chain has instantiated so far (three at creation, plus every StepChunks /
+ * StepResident capture): diagnostics, e.g. to check that steady-state calls replay. */
+GSDR_API size_t gsdrAmChainGraphCaptures(gsdrAmChain chain);
 /* Forget all history: the next step is a first step again. */
 GSDR_API hipError_t gsdrAmChainReset(gsdrAmChain chain);
 

@@ -159,3 +159,73 @@ def test_am_chain_multi_chunk_graph_matches_steps(chain_mod, orc):
     assert got.tobytes() == ref.tobytes()
     want, bound = _expected(orc, iq, rf, D, au, Da)
     assert np.all(np.abs(got - want) <= bound)
+
+
+@pytest.mark.gpu
+def test_am_chain_odd_chunk_batches_replay(chain_mod, orc):
+    """A live stream stepped in batches of an odd number of chunks through the same device buffers:
+    the starting staging parity alternates between calls, and each parity's graph is captured once
+    and then replayed (a single cached graph was recaptured on every call). Output is
+    bit-identical to per-chunk steps."""
+    import torch
+    T, D, Ta, Da, L = 1023, 10, 255, 20, 4000
+    n, calls = 3, 6
+    rng = np.random.default_rng(17)
+    rf = orc.lowpass_taps(T, 0.04)
+    au = orc.lowpass_taps(Ta, 0.02)
+    iq = rng.integers(-128, 128, size=2 * L * n * calls).astype(np.int8)
+    src = torch.from_numpy(iq).cuda()
+    multi = chain_mod.AmChain(rf, D, au, Da, L)
+    base = multi.graph_captures()
+    buf = torch.empty(2 * L * n, dtype=torch.int8, device="cuda")  # the live stream's input buffer
+    out = torch.empty(multi.chunks_output_count(n), dtype=torch.float32, device="cuda")
+    got = []
+    for k in range(calls):
+        multi.torch_stream.synchronize()  # the previous batch read buf in place
+        buf.copy_(src[2 * L * n * k: 2 * L * n * (k + 1)])
+        torch.cuda.synchronize()
+        cnt = multi.step_chunks(buf, n, out)
+        multi.torch_stream.synchronize()
+        got.append(out[:cnt].cpu().numpy().copy())
+    # first step (key 2), then parities 1 and 0 alternate: three captures in all
+    assert multi.graph_captures() - base == 3
+    per = chain_mod.AmChain(rf, D, au, Da, L)
+    ref = np.concatenate([per.step(src[2 * L * s: 2 * L * (s + 1)]).cpu().numpy() for s in range(n * calls)])
+    assert np.concatenate(got).tobytes() == ref.tobytes()
+
+
+@pytest.mark.gpu
+def test_am_chain_reports_ws_abort(chain_mod, orc):
+    """The chain executor's graphs hold the C5 RF stage on the wave-specialised int8 MFMA kernel.
+    With the spin limit at 0 a resident step aborts inside the graph; once the caller has
+    synchronised, the next step fails with hipErrorLaunchTimeOut (graph replays never
+    reported it). With the limit restored the chain recaptures (the limit is a captured argument)
+    and steps correctly again."""
+    import torch
+    from gpusdr import ops
+    from gpusdr._native import HipError
+    T, D, Ta, Da, L = 1023, 10, 255, 20, 1_000_000
+    rng = np.random.default_rng(19)
+    rf = orc.lowpass_taps(T, 0.04)
+    au = orc.lowpass_taps(Ta, 0.02)
+    iq = rng.integers(-128, 128, size=2 * L * 4).astype(np.int8)
+    dev = torch.from_numpy(iq).cuda()
+    assert ops.fir_kernel_class(dev, torch.from_numpy(rf).cuda(), D, int8_iq=True) == "i8-dec-mfma"
+    ops.ws_aborts(reset=True)
+    prev = ops.set_ws_spin_limit(0)
+    try:
+        c = chain_mod.AmChain(rf, D, au, Da, L)
+        out = torch.empty(c.resident_output_count(2), dtype=torch.float32, device="cuda")
+        c.step_resident(dev, 2, out)
+        c.torch_stream.synchronize()
+        with pytest.raises(HipError):
+            c.step_resident(dev[2 * L * 2:], 2, out)
+    finally:
+        ops.set_ws_spin_limit(prev)
+    assert ops.ws_aborts(reset=True) == 0  # the failed step took the count
+    c.reset()
+    base = c.graph_captures()
+    n = c.step_resident(dev, 4, torch.empty(c.resident_output_count(4), dtype=torch.float32, device="cuda"))
+    assert n > 0 and c.graph_captures() > base
+    c.torch_stream.synchronize()
+    assert ops.ws_aborts(reset=True) == 0

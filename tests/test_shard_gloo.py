@@ -1,8 +1,9 @@
-"""Time-sharded streaming (gpusdr/shard.py) with world_size 2 over gloo on the CPU.
+"""Time-sharded streaming (gpusdr/shard.py) with world_size 2, 4 and 8 over gloo on the CPU.
 
 Each rank runs the real ring-halo protocol (HaloRing.step) over torch.distributed; the FIR
 itself is the oracle here (the GPU path runs the same protocol with the HIP kernels in
-bench.py). The concatenated per-rank outputs must equal, bit for bit, one unsharded FIR over
+bench.py). The halos are sent unstaged (HaloRing(stage=False)): the branch RCCL takes with device
+tensors, here with host tensors (gloo cannot move device tensors; the GPU tests stage instead). The concatenated per-rank outputs must equal, bit for bit, one unsharded FIR over
 the whole stream fed (T-1) zeros first - i.e. sharding changes nothing but where work runs.
 """
 import os
@@ -67,10 +68,9 @@ def _run_rank(rank, world, port, D, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("D", [1, 3])
-def test_two_rank_ring_halo_matches_unsharded(tmp_path, orc, D):
+@pytest.mark.parametrize("world,D", [(2, 1), (2, 3), (4, 1), (8, 3)])
+def test_ring_halo_matches_unsharded(tmp_path, orc, world, D):
     import torch.multiprocessing as mp
-    world = 2
     mp.spawn(_run_rank, args=(world, _free_port(), D, str(tmp_path)), nprocs=world, join=True)
     per_rank = [np.load(os.path.join(tmp_path, f"rank{r}.npy")) for r in range(world)]
     sharded = np.concatenate([per_rank[r][s] for s in range(STEPS) for r in range(world)])

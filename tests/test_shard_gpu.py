@@ -1,7 +1,8 @@
-"""Time-sharded streams on the HIP kernels: two ranks (gloo, halos staged through host memory),
-both on cuda:0, run the ring-halo protocol of gpusdr/shard.py with the real gfx950 FIR kernels -
-C4's shape (cf32, 1023 taps, D = 1, bulk / head launches) and the C5 AM receive chain with its
-cascaded halo ((Ta - 1) D + T - 1 samples, AmChainShard). The concatenated per-rank outputs must
+"""Time-sharded streams on the HIP kernels: 2, 4 and 8 ranks (gloo, halos staged through host
+memory), all on cuda:0, run the ring-halo protocol of gpusdr/shard.py with the real gfx950 FIR
+kernels - C4's shape (cf32, 1023 taps, D = 1, bulk / head launches) at the config's 2 and 4 ranks,
+and the C5 AM receive chain with its cascaded halo ((Ta - 1) D + T - 1 samples, AmChainShard) at 2
+and the config's 8 ranks. The concatenated per-rank outputs must
 equal the float64 oracle over the whole stream within the FIR tolerance 1e-6 * sum|h||x|
 (SURVEY.md 8d), i.e. sharding changes nothing but where work runs. The stream is primed: rank 0's
 first halo holds the stream's first samples (as a live receiver's history would), so no window
@@ -18,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIR_TOL = 1e-6
-WORLD, STEPS = 2, 3
+STEPS = 3
 
 
 def _free_port():
@@ -80,18 +81,19 @@ def _rank_main(rank, world, port, kind, out_dir):
     dist.destroy_process_group()
 
 
-def _run(kind, tmp_path):
+def _run(kind, tmp_path, world):
     import torch.multiprocessing as mp
-    mp.start_processes(_rank_main, args=(WORLD, _free_port(), kind, str(tmp_path)), nprocs=WORLD, join=True,
+    mp.start_processes(_rank_main, args=(world, _free_port(), kind, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
-    per = [np.load(os.path.join(tmp_path, f"{kind}_rank{r}.npy")) for r in range(WORLD)]
-    return np.concatenate([per[r][s] for s in range(STEPS) for r in range(WORLD)])
+    per = [np.load(os.path.join(tmp_path, f"{kind}_rank{r}.npy")) for r in range(world)]
+    return np.concatenate([per[r][s] for s in range(STEPS) for r in range(world)])
 
 
-def test_c4_shape_time_sharded_on_hip(tmp_path, orc):
+@pytest.mark.parametrize("world", [2, 4])
+def test_c4_shape_time_sharded_on_hip(tmp_path, orc, world):
     T, D, L = 1023, 1, 20_000
-    got = _run("c4", tmp_path)
-    n = L * WORLD * STEPS
+    got = _run("c4", tmp_path, world)
+    n = L * world * STEPS
     stream = orc.synth_wideband_cf32(0xC4, 0.013, 0.31, 0, T - 1 + n)
     y64, bound = orc.fir_f64(orc.lowpass_taps(T, 0.04, "blackman"), stream, D, n // D)
     assert len(got) == len(y64)
@@ -99,20 +101,21 @@ def test_c4_shape_time_sharded_on_hip(tmp_path, orc):
     assert np.all(err <= FIR_TOL * bound + 1e-30), float(np.max(err / (bound + 1e-30)))
 
 
-def test_c5_chain_time_sharded_cascaded_halo(tmp_path, orc):
+@pytest.mark.parametrize("world", [2, 8])
+def test_c5_chain_time_sharded_cascaded_halo(tmp_path, orc, world):
     from gpusdr.shard import ChainShardGeometry
     T, D, Ta, Da, L = 1023, 10, 255, 20, 40_000
-    H = ChainShardGeometry(0, WORLD, L, T, D, Ta, Da).halo
+    H = ChainShardGeometry(0, world, L, T, D, Ta, Da).halo
     assert H == 3600  # (Ta - 1) D + T - 1 = 3562, rounded up to a multiple of D Da
-    got = _run("c5", tmp_path)
-    padded = orc.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, H + L * WORLD * STEPS)  # primed stream
+    got = _run("c5", tmp_path, world)
+    padded = orc.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, H + L * world * STEPS)  # primed stream
     rf, au = orc.lowpass_taps(T, 0.04, "blackman"), orc.lowpass_taps(Ta, 0.02)
     x = orc.int8_to_float(padded).view(np.complex64)
     y, rf_bound = orc.fir_f64(rf, x, D)
     am = np.abs(y)
     want, audio_bound = orc.fir_f64(au, am.astype(np.float32), Da)
     n = len(got)
-    assert n == L * WORLD * STEPS // (D * Da) and len(want) >= n
+    assert n == L * world * STEPS // (D * Da) and len(want) >= n
     carried, _ = orc.fir_f64(np.abs(au), (FIR_TOL * (rf_bound + am)).astype(np.float32), Da, n)
     bound = carried + FIR_TOL * audio_bound[:n] + 1e-30
     assert np.all(np.abs(got - want[:n]) <= bound)

@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define DECL(N)                                                                                        \
@@ -216,6 +217,27 @@ int main() {
     }
     hipMemcpy(taps, ht.data(), sh.T * 4, hipMemcpyHostToDevice);
     if (!sh.i8 && getenv("FFT_BENCH_READBW")) readBw(x, inBytes);
+    // FFT_BENCH_LOOP=<variant name>: loop that variant for FFT_BENCH_REPS launches (power / clock
+    // probes sample amd-smi meanwhile), printing the mean launch time every 2000 launches
+    if (const char* lv = getenv("FFT_BENCH_LOOP")) {
+      if (sh.i8 || sh.D == 1) { hipFree(x); hipFree(taps); hipFree(out); hipFree(ref); continue; }
+      const int reps = getenv("FFT_BENCH_REPS") ? atoi(getenv("FFT_BENCH_REPS")) : 20000;
+      for (int v = 0; v < nv; ++v) {
+        if (strcmp(vars[v].name, lv) != 0) continue;
+        for (int r0 = 0; r0 < reps; r0 += 2000) {
+          hipEventRecord(e0);
+          for (int r = 0; r < 2000; ++r) vars[v].fn(x, sh.i8, taps, sh.T, sh.D, out, nOut, 2, 0);
+          hipEventRecord(e1);
+          hipEventSynchronize(e1);
+          float ms = 0;
+          hipEventElapsedTime(&ms, e0, e1);
+          printf("loop %-10s %6d launches  %8.1f us/launch\n", lv, r0 + 2000, ms * 1e3 / 2000);
+          fflush(stdout);
+        }
+      }
+      hipFree(x); hipFree(taps); hipFree(out); hipFree(ref);
+      continue;
+    }
     std::vector<float> a(nOut), b(nOut);
     // correctness: every variant's output against the first
     std::vector<double> md(nv, 0.0);
