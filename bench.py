@@ -56,10 +56,14 @@ WORKLOADS = {
            "c64", (1 << 28) - (1 << 28) % 10, 1023, 10, 0.04, "blackman", 200e6),
     "c4": ("C4: cf32 stream, 1023-tap FC FIR, D=1 -> QuadAmDemod, 2^26 samples per GPU step",
            "c64", 1 << 26, 1023, 1, 0.04, "blackman", 1e9),
+    "c4s": ("C4 (strong scaling): one 2^30-sample cf32 stream per step, 1023-tap FC FIR, D=1 -> QuadAmDemod, "
+            "time-sharded over the N GPUs (2^30 / N samples per GPU step)",
+            "c64", 1 << 30, 1023, 1, 0.04, "blackman", 1e9),
     "c5": ("C5: full AM chain @1 Gsps (1/8 per GPU): int8 IQ -> 1023-tap FC FIR, D=10 -> AM -> 255-tap FF "
-           "FIR, D=20, 125 M samples (1 s) per GPU step, hipGraph-captured",
+           "FIR, D=20, 125 M samples (1 s) per GPU step",
            "i8", 125_000_000, 1023, 10, 0.04, "blackman", 1e9),
 }
+STRONG = {"c4s"}  # workloads whose samples per step are the WHOLE job's, split over the ranks
 C5_CHUNK = 5_000_000   # multiple of D * Da = 200
 C5_AUDIO = (255, 20, 0.02, "hamming")
 
@@ -118,6 +122,8 @@ class ShardedChain:
     def __init__(self, ops, wl, rank, world, device, stage=False):
         from gpusdr.shard import HaloRing, ShardGeometry
         desc, kind, L, T, D, cutoff, window, fs = WORKLOADS[wl]
+        if wl in STRONG:  # the job's fixed stream per step, split over the ranks
+            L = L // world // D * D
         self.ops, self.kind, self.L, self.T, self.D = ops, kind, L, T, D
         self.geom = g = ShardGeometry(rank, world, L, T, D)
         H = g.halo
@@ -469,6 +475,122 @@ def spawn_ranks(n, share_gpu=False):
                        start_method="spawn")
 
 
+def timed_steps(chain, steps, warmup, world, backend, device, local, ops):
+    """W untimed steps, then K steps between barrier + synchronize on both sides; the max over ranks
+    of the wall time, and the mean per-step HIP-event time of the timed kernel."""
+    for _ in range(warmup):
+        chain.step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    ops.fft_direct_blocks(local, reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        chain.step(evs[i])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    return elapsed, kernel_ms, ops.fft_direct_blocks(local, reset=True)
+
+
+def extra_line(wl, chain, elapsed, kernel_ms, steps, world):
+    """A secondary workload measured in the same run (same protocol as the headline)."""
+    bytes_, (kind, fl, peak) = chain.timed_bytes_ops()
+    gbs = bytes_ / (kernel_ms * 1e-3) / 1e9
+    strong = wl in STRONG
+    return {"workload": WORKLOADS[wl][0], "value": world * chain.L * steps / elapsed / 1e6, "unit": "Msamples/s",
+            "n_gpus": world, "steps": steps, "ms_per_step": elapsed / steps * 1e3,
+            "scaling": "strong" if strong else "weak", "samples_per_gpu_step": chain.L,
+            "kernel": kernel_name(chain), "kernel_class": chain.kernel_class,
+            "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS, "avg_launch_ms": kernel_ms,
+            "algorithmic_bytes_per_launch": bytes_}
+
+
+def node_path(ops, device, kernel_value, segments=5, warmup=1):
+    """C3 through the reference's filter-graph API (getFactoriesSingleton nodes, SteppingDriver):
+    Fir(real taps, FloatComplex, D = 10) -> QuadAmDemod -> a device sink taking one C3 segment of AM
+    output per step. The Fir window is pre-filled with `segments` C3 segments (2^28 - 6 samples each,
+    outside the timed region: an upstream node would write them there); each driver step then moves
+    one segment: with fusion ONE gsdrFirFCAmDemod launch, without it the reference's Fir and
+    QuadAmDemod launches with the cf32 intermediate in the AM window. Also the host time of one
+    driver step, eager vs replayed (doFilterGraphed), on 1 MiB pushes (the reference's chunk)."""
+    from gpusdr import graph
+    desc, kind, L, T, D, cutoff, window, fs = WORKLOADS["c3"]
+    taps = lowpass(T, cutoff, window)
+    n_out = (L - T) // D + 1
+    out = {"workload": "C3 through the filter-graph nodes: Fir(Float taps, FloatComplex, D=10) -> QuadAmDemod -> "
+                       "device sink, SteppingDriver.doFilter, one 2^28-sample segment per step",
+           "kernel_line_msps": kernel_value}
+    steps = segments - warmup
+    for fuse in (True, False):
+        q = graph.Queue(device.index)
+        fir = graph.Node.fir(q, taps, D, graph.SAMPLE_FLOAT_COMPLEX)
+        am = graph.Node.quad_am_demod(q)
+        sink = graph.Node.device_sink(q, n_out * 4)
+        drv = graph.SteppingDriver()
+        drv.set_fuse_fir_am(fuse)
+        drv.connect(fir, 0, am, 0)
+        drv.connect(am, 0, sink, 0)
+        n_in = segments * n_out * D + T - D
+        x = torch.empty(n_in, dtype=torch.complex64, device=device)
+        ops.synth_wideband_cf32(0xC3, 0.013, 0.31, 0, n_in, out=x)
+        torch.cuda.synchronize()
+        fir.push_device(x.data_ptr(), x.numel() * 8)
+        q.sync()
+        del x
+        for _ in range(warmup):
+            drv.do_filter()
+        q.sync()
+        # outputs delivered in the timed steps: the Fir's outputs consumed minus what still waits in
+        # the AM window (unfused steps need not line up with segments)
+        fir0, am0 = fir.output_size()[0] // 8, am.output_size()[0] // 4
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            drv.do_filter()
+        q.sync()
+        dt = (time.perf_counter() - t0) / steps
+        done = (fir0 - fir.output_size()[0] // 8) - (am.output_size()[0] // 4 - am0)
+        msps = done * D / steps / dt / 1e6
+        st = drv.graph_stats()
+        key = "fused" if fuse else "unfused"
+        out[key] = {"value": msps, "unit": "Msamples/s", "ms_per_step": dt * 1e3,
+                    "outputs_per_step": done / steps, "fused_edges": st["fused"],
+                    "vs_kernel_line": msps / kernel_value}
+        del drv, sink, am, fir
+        torch.cuda.empty_cache()
+    # host cost of a driver step at the reference's 1 MiB chunk: eager vs graph replay
+    q = graph.Queue(device.index)
+    chunk = 131_070  # cf32 samples, a multiple of D: the chain's state repeats
+    xs = torch.empty(chunk, dtype=torch.complex64, device=device)
+    ops.synth_wideband_cf32(0xC3, 0.013, 0.31, 0, chunk, out=xs)
+    host = {}
+    for mode in ("eager", "graphed"):
+        fir = graph.Node.fir(q, taps, D, graph.SAMPLE_FLOAT_COMPLEX)
+        am = graph.Node.quad_am_demod(q)
+        sink = graph.Node.device_sink(q, 0)
+        drv = graph.SteppingDriver()
+        drv.connect(fir, 0, am, 0)
+        drv.connect(am, 0, sink, 0)
+        ts = []
+        for i in range(60):
+            fir.push_device(xs.data_ptr(), chunk * 8)
+            t0 = time.perf_counter()
+            drv.do_filter() if mode == "eager" else drv.do_filter_graphed(q)
+            ts.append(time.perf_counter() - t0)
+            q.sync()
+        host[mode] = {"host_us_per_step": float(np.median(ts[30:])) * 1e6, **drv.graph_stats()}
+    out["host_step_1MiB"] = host
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -485,6 +607,9 @@ def main():
                          "halos through host memory)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="run every rank on cuda:0 (testing the multi-rank path on a one-GPU box; gloo)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the secondary measurements (C4 strong scaling, C5, the C3 node path) that the "
+                         "default run adds to its JSON line under 'extras'")
     args = ap.parse_args()
     if args.share_gpu and args.backend != "gloo":
         raise SystemExit("bench.py: --share-gpu needs --backend gloo (RCCL runs one rank per GPU)")
@@ -502,34 +627,37 @@ def main():
     else:
         chain = ShardedChain(ops, args.workload, rank, world, device, stage)
 
-    for _ in range(args.warmup):
-        chain.step()
-    torch.cuda.synchronize()
-
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    ops.fft_direct_blocks(local, reset=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        chain.step(evs[i])
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    direct_blocks = ops.fft_direct_blocks(local, reset=True)  # FFT blocks the accuracy guard sent to the direct form
+    elapsed, kernel_ms, direct_blocks = timed_steps(chain, args.steps, args.warmup, world, args.backend, device,
+                                                    local, ops)
     bytes_, (compute_kind, ops_, peak_t) = chain.timed_bytes_ops()
     achieved_gbs = bytes_ / (kernel_ms * 1e-3) / 1e9
     achieved_t = ops_ / (kernel_ms * 1e-3) / 1e12
     total_samples = world * chain.L * args.steps
     value = total_samples / elapsed / 1e6
+
+    # secondary workloads in the same run, so the driver's 1/2/4/8-GPU runs measure every config
+    # BASELINE.json names: C4 as stated (one 2^30-sample stream split over the GPUs, strong scaling),
+    # the C5 chain, and (N = 1) C3 through the reference's node API
+    extras = {}
+    if args.workload == "c3" and not args.no_extras:
+        chain_info = (chain.kernel_class, kernel_name(chain), chain.L, chain.T, chain.D, chain.kind, chain.geom,
+                      getattr(chain, "n_slots", 1))
+        del chain
+        torch.cuda.empty_cache()
+        for wl, k, w in (("c4s", 6, 2), ("c5", 20, 3)):
+            xc = (AmChainSharded(ops, rank, world, device, stage) if wl == "c5" else
+                  ShardedChain(ops, wl, rank, world, device, stage))
+            e2, k2, _ = timed_steps(xc, k, w, world, args.backend, device, local, ops)
+            extras[wl] = extra_line(wl, xc, e2, k2, k, world)
+            del xc
+            torch.cuda.empty_cache()
+        if world == 1:
+            extras["c3_nodes"] = node_path(ops, device, value)
+        chain = argparse.Namespace(kernel_class=chain_info[0], L=chain_info[2], T=chain_info[3], D=chain_info[4],
+                                   kind=chain_info[5], geom=chain_info[6], n_slots=chain_info[7])
+        kernel_label = chain_info[1]
+    else:
+        kernel_label = kernel_name(chain)
 
     if rank == 0:
         desc = WORKLOADS[args.workload][0]
@@ -549,7 +677,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.workload in STRONG else "weak",
             "vs_baseline": None,
             "dtype": "f32",  # complex float32 samples / fp32 accumulation; the arithmetic form:
             "arithmetic": compute_kind,
@@ -572,7 +700,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": kernel_name(chain),
+                "kernel": kernel_label,
                 "achieved": achieved_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -587,6 +715,7 @@ def main():
                 "fft_direct_blocks": direct_blocks,
             },
             "cpu_baseline": cpu,
+            **({"extras": extras} if extras else {}),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -185,6 +185,12 @@ uint32_t gspHostBufferCreate(gspHandle queue, size_t bytes, gspHandle* bufferOut
   return give(bf.get()->createBuffer(bytes), bufferOut);
 }
 
+uint32_t gspDeviceSinkCreate(gspHandle queue, size_t preferredBytes, gspHandle* sinkOut) {
+  ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
+  if (q == nullptr) return Status_InvalidArgument;
+  return give(gsdr_rt::DeviceSink::create(preferredBytes, q, factories()), sinkOut);
+}
+
 uint32_t gspHostSinkCreate(gspHandle queue, gspHandle* sinkOut) {
   ICudaCommandQueue* q = as<ICudaCommandQueue>(queue);
   if (q == nullptr) return Status_InvalidArgument;
@@ -299,6 +305,20 @@ uint32_t gspDriverGraphStats(gspHandle driver, size_t* eager, size_t* captured, 
   if (eager) *eager = st.eager;
   if (captured) *captured = st.captured;
   if (replayed) *replayed = st.replayed;
+  return Status_Success;
+}
+
+uint32_t gspDriverSetFuseFirAm(gspHandle driver, int32_t on) {
+  auto* d = dynamic_cast<gsdr_rt::SteppingDriver*>(as<IDriver>(driver));
+  if (d == nullptr) return Status_InvalidArgument;
+  d->setFuseFirAm(on != 0);
+  return Status_Success;
+}
+
+uint32_t gspDriverFusedSteps(gspHandle driver, size_t* fused) {
+  auto* d = dynamic_cast<gsdr_rt::SteppingDriver*>(as<IDriver>(driver));
+  if (d == nullptr || fused == nullptr) return Status_InvalidArgument;
+  *fused = d->graphStats().fused;
   return Status_Success;
 }
 

@@ -163,6 +163,15 @@ Status SteppingDriver::doSinkInput(Sink* sink, int depth) {
       gslogt("Sink [%s] port [%zu] does not have a Source connected to it", nameOf(sink), port);
       continue;
     }
+    if (Fir* fir = fusableFirAm(up.source)) {  // Fir -> QuadAmDemod in one launch
+      if (fir->fusedAmOutputBytes() == 0) {
+        FWD_IF_ERR(doSinkInput(fir, depth + 1));
+        if (fir->fusedAmOutputBytes() == 0) return Status_Success;
+      }
+      FWD_IF_ERR(doSourceOutput(up.source, fir));
+      ++mStats.fused;
+      continue;
+    }
     Sink* upstreamSink = up.source->asSink();
     if (upstreamSink != nullptr && !hasDataForAllPorts(up.source)) {
       FWD_IF_ERR(doSinkInput(upstreamSink, depth + 1));
@@ -173,11 +182,28 @@ Status SteppingDriver::doSinkInput(Sink* sink, int depth) {
   return Status_Success;
 }
 
+// The Fir feeding `source` when `source` is a QuadAmDemod the driver may step together with it: the
+// AM window is empty (nothing of an unfused step left to demodulate), its one input is fed by a
+// Fir with real taps whose only sink it is, both on one stream.
+Fir* SteppingDriver::fusableFirAm(Source* source) {
+  if (!mFuseFirAm) return nullptr;
+  auto* am = dynamic_cast<QuadAmDemod*>(source);
+  if (am == nullptr || !am->inputEmpty() || mSources.find(source) == mSources.end()) return nullptr;
+  auto it = mSinks.find(am);
+  if (it == mSinks.end() || it->second.inputs.size() != 1 || it->second.inputs[0].port != 0) return nullptr;
+  auto* fir = dynamic_cast<Fir*>(it->second.inputs[0].source);
+  if (fir == nullptr || !fir->canFuseAm() || fir->stream() != am->stream()) return nullptr;
+  auto fs = mSources.find(fir);
+  if (fs == mSources.end() || fs->second.ports.size() != 1 || fs->second.ports[0].size() != 1) return nullptr;
+  return fir;
+}
+
 // SteppingDriver.cpp:247-366: each connected sink lends a buffer sized
 // alignUp(min(sink preferred, source available), source alignment); the first sink of a port
 // receives readOutput's data, further sinks of the same port get a copy through the source's
-// output copier; then every sink commits the bytes written.
-Status SteppingDriver::doSourceOutput(Source* source) {
+// output copier; then every sink commits the bytes written. With `fusedFir` (source is the
+// QuadAmDemod it feeds, fusableFirAm) the data comes from the fused FIR + AM launch instead.
+Status SteppingDriver::doSourceOutput(Source* source, Fir* fusedFir) {
   SourceInfo& si = mSources.at(source);
   const size_t nPorts = si.ports.size();
   for (size_t p = 0; p < nPorts; ++p) {
@@ -200,7 +226,7 @@ Status SteppingDriver::doSourceOutput(Source* source) {
   for (size_t p = 0; p < nPorts; ++p) {
     size_t alignment = source->getOutputSizeAlignment(p);
     if (alignment == 0) alignment = 1;
-    const size_t available = source->getOutputDataSize(p);
+    const size_t available = fusedFir != nullptr ? fusedFir->fusedAmOutputBytes() : source->getOutputDataSize(p);
     for (const SinkPortKey& k : si.ports[p]) {
       const size_t want = std::min(k.sink->preferredInputBufferSize(k.port), available);
       const size_t bytes = want > SIZE_MAX - alignment + 1 ? want / alignment * alignment
@@ -242,7 +268,7 @@ Status SteppingDriver::doSourceOutput(Source* source) {
       mViewRefs.emplace_back(std::move(view));
     }
   }
-  Status st = source->readOutput(mPortBuffers.data(), nPorts);
+  Status st = fusedFir != nullptr ? fusedFir->readOutputAm(mPortBuffers[0]) : source->readOutput(mPortBuffers.data(), nPorts);
   if (st != Status_Success) {
     gsloge("Source [%s] readOutput failed [%u]", nameOf(source), (unsigned)st);
     cancel(mBufferRefs.size());

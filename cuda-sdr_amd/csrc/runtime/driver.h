@@ -17,6 +17,7 @@
 
 #include <gpusdrpipeline/Factories.h>
 
+#include "filters.h"
 #include "graph_state.h"
 
 #include <hip/hip_runtime_api.h>
@@ -54,8 +55,15 @@ class SteppingDriver final : public ISteppingDriver {
     size_t eager = 0;     // steps run as plain launches
     size_t captured = 0;  // steps that captured (and launched) a new graph
     size_t replayed = 0;  // steps whose device work was a cached graph launch
+    size_t fused = 0;     // Fir -> QuadAmDemod edges moved as one fused launch
   };
   GraphStats graphStats() const noexcept { return mStats; }
+
+  // MI355X: a Fir (real taps, cf32 or int8 IQ input) whose only sink is a QuadAmDemod on the same
+  // stream is stepped together with it - ONE gsdrFirFCAmDemod launch writes |y| straight into the
+  // QuadAmDemod's downstream buffer, so the cf32 FIR output never goes through HBM and the AM node's
+  // launch disappears (bit-identical output; the AM node's window stays empty). On by default.
+  void setFuseFirAm(bool on) noexcept { mFuseFirAm = on; }
 
  private:
   struct SinkPortKey {
@@ -87,7 +95,8 @@ class SteppingDriver final : public ISteppingDriver {
   const char* nameOf(Node* node) const noexcept;
   bool hasDataForAllPorts(Source* source);
   Status doSinkInput(Sink* sink, int depth);
-  Status doSourceOutput(Source* source);
+  Status doSourceOutput(Source* source, Fir* fusedFir = nullptr);
+  Fir* fusableFirAm(Source* source);
 
   // std::unordered_map keeps element addresses stable across inserts (references handed out above)
   std::unordered_map<Source*, SourceInfo> mSources;
@@ -115,6 +124,7 @@ class SteppingDriver final : public ISteppingDriver {
   GraphStats mStats;
   hipEvent_t mGraphDone = nullptr;  // after the last graph launch: wave-specialised aborts settle
   bool mGraphLaunched = false;
+  bool mFuseFirAm = true;
   bool chainState(hipStream_t stream, uint64_t& key, std::vector<IGraphStepState*>* nodesOut) const noexcept;
   Status captureStep(hipStream_t stream, hipGraph_t* graphOut) noexcept;
   Status launchGraph(hipGraphExec_t exec, hipStream_t stream) noexcept;

@@ -159,6 +159,26 @@ Status Fir::readOutput(IBuffer** portOutputBuffers, size_t portCount) noexcept {
   return consumeInputBytesAndMoveUsedToStart(0, n * mDecimation * mInElem);
 }
 
+Status Fir::readOutputAm(IBuffer* out) noexcept {
+  GS_REQUIRE_OR_RET_STATUS(out != nullptr && canFuseAm(), "Fir::readOutputAm needs real taps and an output");
+  Ref<IBuffer> in;
+  UNWRAP_OR_FWD_STATUS(in, getPortInputBuffer(0));
+  const size_t n = std::min(availableOutputs(), out->range()->remaining() / sizeof(float));
+  if (n == 0) return Status_Success;
+  const int32_t dev = mQueue->cudaDevice();
+  hipStream_t s = mQueue->cudaStream();
+  hipError_t e;
+  if (mElementType == SampleType_Int8Complex)
+    e = gsdrInt8FirFCAmDemod(mDecimation, mTaps->as<float>(), mTapCount, in->readPtr<int8_t>(), out->writePtr<float>(),
+                             n, dev, s);
+  else
+    e = gsdrFirFCAmDemod(mDecimation, mTaps->as<float>(), mTapCount, in->readPtr<hipFloatComplex>(),
+                         out->writePtr<float>(), n, dev, s);
+  SAFE_HIP_OR_RET_STATUS(e);
+  FWD_IF_ERR(out->range()->increaseEndOffset(n * sizeof(float)));
+  return consumeInputBytesAndMoveUsedToStart(0, n * mDecimation * mInElem);
+}
+
 // ---- QuadAmDemod (QuadAmDemod.cpp:31-109) ------------------------------------------------------------
 Result<Filter> QuadAmDemod::create(ICudaCommandQueue* queue, IFactories* factories) noexcept {
   NON_NULL_PARAM_OR_RET(queue);
@@ -182,6 +202,12 @@ size_t QuadAmDemod::getOutputDataSize(size_t port) noexcept {
   Result<IBuffer> in = getPortInputBuffer(0);
   if (in.status != Status_Success) return 0;
   return in.value->range()->used() / (2 * sizeof(float)) * sizeof(float);
+}
+
+bool QuadAmDemod::inputEmpty() const noexcept {
+  if (!inputPortsInitialized()) return true;
+  Result<const IBuffer> in = getPortInputBuffer(0);
+  return in.status == Status_Success && in.value->range()->used() == 0;
 }
 
 size_t QuadAmDemod::getOutputSizeAlignment(size_t port) noexcept {
@@ -463,6 +489,26 @@ Status HipMemcpyFilter::readOutput(IBuffer** portOutputBuffers, size_t portCount
 }
 
 // ---- host egress (AacFileWriter.cpp:267-280 minus the codec; Waiter.cpp:34-50) ---------------------------
+Result<Sink> DeviceSink::create(size_t preferredBytes, ICudaCommandQueue* queue, IFactories* factories) noexcept {
+  NON_NULL_PARAM_OR_RET(queue);
+  Ref<IRelocatableResizableBufferFactory> windows;
+  UNWRAP_OR_FWD_RESULT(windows, factories->createRelocatableCudaBufferFactory(queue, 32, false));
+  return makeRefResultNonNull<Sink>(new (std::nothrow) DeviceSink(
+      preferredBytes == 0 ? kDevicePreferredBytes : preferredBytes, windows.get().get(),
+      factories->getBufferSliceFactory(), queue));
+}
+
+DeviceSink::DeviceSink(size_t preferredBytes, IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
+                       ICudaCommandQueue* queue) noexcept
+    : BaseSink(windows, slices, 1), mQueue(queue), mPreferred(preferredBytes) {}
+
+Status DeviceSink::commitBuffer(size_t port, size_t byteCount) noexcept {
+  FWD_IF_ERR(BaseSink::commitBuffer(port, byteCount));
+  Ref<IBuffer> in;
+  UNWRAP_OR_FWD_STATUS(in, getPortInputBuffer(port));
+  return consumeInputBytesAndMoveUsedToStart(port, in->range()->used());
+}
+
 Result<Sink> HostEgressSink::create(ICudaCommandQueue* queue, IFactories* factories) noexcept {
   NON_NULL_PARAM_OR_RET(queue);
   Ref<IRelocatableResizableBufferFactory> windows;

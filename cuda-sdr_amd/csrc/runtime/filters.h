@@ -15,6 +15,13 @@
 
 namespace gsdr_rt {
 
+// Preferred input window of the device filters on MI355X. The reference asks for 1 MiB per step
+// (Fir.cpp:311, QuadAmDemod.cpp:107), i.e. 131 072 cf32 samples: at C3's shape that is ~32 FFT
+// blocks for 256 CUs x 8 waves, and every step pays its launches, so a driver-stepped chain ran at a
+// fraction of the kernel rate. 256 MiB (33.5 M cf32 samples, several rounds of blocks on every CU)
+// is cheap against 288 GB of HBM. The host staging filter keeps 1 MiB (PCIe transfers).
+constexpr size_t kDevicePreferredBytes = size_t{256} << 20;
+
 // Bytes per element of each SampleType on a filter's *input* side. Int8Complex is one I/Q
 // pair (2 bytes); the reference's 1-byte size (Fir.cpp:34-45) never produced output.
 size_t inputElementSize(SampleType t) noexcept;
@@ -35,10 +42,22 @@ class Fir final : public BaseFilter, public IGraphStepState {
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
   Status readOutput(IBuffer** portOutputBuffers, size_t numPorts) noexcept final;
-  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+  size_t preferredInputBufferSize(size_t port) noexcept final { return kDevicePreferredBytes; }
 
   size_t decimation() const noexcept { return mDecimation; }
   size_t tapCount() const noexcept { return mTapCount; }
+
+  // MI355X: the FIR and the AM envelope of a QuadAmDemod it feeds as ONE launch
+  // (gsdrFirFCAmDemod / gsdrInt8FirFCAmDemod, bit-identical to gsdrFirFC + gsdrQuadAmDemod): the
+  // envelope |y| goes straight into `out` (floats) and the cf32 outputs never touch HBM
+  // (SteppingDriver fuses Fir -> QuadAmDemod edges, driver.cpp). Real taps only.
+  bool canFuseAm() const noexcept {
+    return mTapType == SampleType_Float &&
+           (mElementType == SampleType_FloatComplex || mElementType == SampleType_Int8Complex);
+  }
+  size_t fusedAmOutputBytes() const noexcept { return availableOutputs() * sizeof(float); }
+  Status readOutputAm(IBuffer* out) noexcept;
+  hipStream_t stream() const noexcept { return mQueue->cudaStream(); }
 
  private:
   Fir(SampleType tapType, SampleType elementType, size_t decimation, ICudaCommandQueue* queue, IAllocator* allocator,
@@ -75,7 +94,9 @@ class QuadAmDemod final : public BaseFilter, public IGraphStepState {
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
   Status readOutput(IBuffer** portOutputBuffers, size_t numPorts) noexcept final;
-  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+  size_t preferredInputBufferSize(size_t port) noexcept final { return kDevicePreferredBytes; }
+  bool inputEmpty() const noexcept;  // no cf32 left in the window (fusion keeps it empty)
+  hipStream_t stream() const noexcept { return mQueue->cudaStream(); }
 
  private:
   QuadAmDemod(ICudaCommandQueue* queue, IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
@@ -124,7 +145,7 @@ class QuadFmDemod final : public BaseFilter, public IGraphStepState {
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
   Status readOutput(IBuffer** portOutputBuffers, size_t portCount) noexcept final;
-  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+  size_t preferredInputBufferSize(size_t port) noexcept final { return kDevicePreferredBytes; }
 
  private:
   QuadFmDemod(float gain, ICudaCommandQueue* queue, IRelocatableResizableBufferFactory* windows,
@@ -148,7 +169,7 @@ class Int8ToFloat final : public BaseFilter, public IGraphStepState {
   size_t getOutputDataSize(size_t port) noexcept final;
   size_t getOutputSizeAlignment(size_t port) noexcept final;
   Status readOutput(IBuffer** portOutputBuffers, size_t numPorts) noexcept final;
-  size_t preferredInputBufferSize(size_t port) noexcept final { return 1 << 20; }
+  size_t preferredInputBufferSize(size_t port) noexcept final { return kDevicePreferredBytes; }
 
  private:
   Int8ToFloat(ICudaCommandQueue* queue, IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
@@ -203,6 +224,30 @@ class HipMemcpyFilter final : public BaseFilter, public IGraphStepState {
   ConstRef<IBufferCopier> mCopier;
   ConstRef<ICudaCommandQueue> mQueue;
   REF_COUNTED(HipMemcpyFilter);
+};
+
+// A device-memory sink that retires every committed byte (the consumer of a benchmarked chain, or
+// any graph tail whose output is not read back): its window never grows past one step.
+class DeviceSink final : public BaseSink, public IGraphStepState {
+ public:
+  hipStream_t graphStream() const noexcept final { return mQueue->cudaStream(); }
+  bool graphState(uint64_t& h) const noexcept final {
+    foldWindowState(h);
+    h = (h ^ mPreferred) * 0x100000001B3ull;
+    return true;
+  }
+  bool saveStepState(GraphNodeState& out) const noexcept final { return saveSinkWindows(*this, out); }
+  Status restoreStepState(const GraphNodeState& in) noexcept final { return restoreSinkWindows(*this, in); }
+  static Result<Sink> create(size_t preferredBytes, ICudaCommandQueue* queue, IFactories* factories) noexcept;
+  Status commitBuffer(size_t port, size_t byteCount) noexcept final;
+  size_t preferredInputBufferSize(size_t port) noexcept final { return mPreferred; }
+
+ private:
+  DeviceSink(size_t preferredBytes, IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
+             ICudaCommandQueue* queue) noexcept;
+  ConstRef<ICudaCommandQueue> mQueue;
+  const size_t mPreferred;
+  REF_COUNTED(DeviceSink);
 };
 
 // Egress: the host end of a chain (reference AacFileWriter.cpp:267-280 minus the codec, with the

@@ -54,6 +54,9 @@ def _L():
             "gspBufferCreate": ([h, sz, ph], u32),
             "gspHostBufferCreate": ([h, sz, ph], u32),
             "gspHostSinkCreate": ([h, ph], u32),
+            "gspDeviceSinkCreate": ([h, sz, ph], u32),
+            "gspDriverSetFuseFirAm": ([h, ctypes.c_int32], u32),
+            "gspDriverFusedSteps": ([h, psz], u32),
             "gspHostSinkAvailable": ([h, psz], u32),
             "gspHostSinkRead": ([h, vp, sz, psz], u32),
             "gspHostSinkFlush": ([h], u32),
@@ -217,6 +220,12 @@ class Node(_Handle):
         """The host egress sink (gspHostSinkCreate): one step in flight, the rest in a host FIFO."""
         return cls(_create(_L().gspHostSinkCreate, queue.handle, what="gspHostSinkCreate"), queue)
 
+    @classmethod
+    def device_sink(cls, queue: Queue, preferred_bytes: int = 0):
+        """A device sink that retires every committed byte (gspDeviceSinkCreate)."""
+        return cls(_create(_L().gspDeviceSinkCreate, queue.handle, preferred_bytes, what="gspDeviceSinkCreate"),
+                   queue)
+
     def host_available(self):
         n = ctypes.c_size_t()
         _check(_L().gspHostSinkAvailable(self._h, ctypes.byref(n)), "hostSinkAvailable")
@@ -302,6 +311,11 @@ class SteppingDriver(_Handle):
         _check(_L().gspDriverDoFilterGraphed(self._h, queue.handle), "doFilterGraphed")
 
     def graph_stats(self):
-        e, c, r = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        e, c, r, f = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
         _check(_L().gspDriverGraphStats(self._h, ctypes.byref(e), ctypes.byref(c), ctypes.byref(r)), "graphStats")
-        return {"eager": e.value, "captured": c.value, "replayed": r.value}
+        _check(_L().gspDriverFusedSteps(self._h, ctypes.byref(f)), "fusedSteps")
+        return {"eager": e.value, "captured": c.value, "replayed": r.value, "fused": f.value}
+
+    def set_fuse_fir_am(self, on: bool):
+        """Fir -> QuadAmDemod as one fused launch (default on; off = the reference's two launches)."""
+        _check(_L().gspDriverSetFuseFirAm(self._h, 1 if on else 0), "setFuseFirAm")

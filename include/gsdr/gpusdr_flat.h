@@ -76,6 +76,9 @@ GSP_API uint32_t gspHostBufferCreate(gspHandle queue, size_t bytes, gspHandle* b
  * gspHostSinkRead drains up to `capacity` bytes (count in *bytesOut); gspHostSinkFlush waits for the
  * in-flight step and queues it too. */
 GSP_API uint32_t gspHostSinkCreate(gspHandle queue, gspHandle* sinkOut);
+/* A device sink that retires every committed byte (a chain's consumer in benchmarks, or a tail
+ * whose output is not read back); it asks for preferredBytes per step (0: 256 MiB). */
+GSP_API uint32_t gspDeviceSinkCreate(gspHandle queue, size_t preferredBytes, gspHandle* sinkOut);
 GSP_API uint32_t gspHostSinkAvailable(gspHandle sink, size_t* bytesOut);
 GSP_API uint32_t gspHostSinkRead(gspHandle sink, void* dst, size_t capacity, size_t* bytesOut);
 GSP_API uint32_t gspHostSinkFlush(gspHandle sink);
@@ -104,6 +107,11 @@ GSP_API uint32_t gspDriverDoFilter(gspHandle driver);
  * gspDriverGraphStats counts plain, capturing and replayed steps. */
 GSP_API uint32_t gspDriverDoFilterGraphed(gspHandle driver, gspHandle queue);
 GSP_API uint32_t gspDriverGraphStats(gspHandle driver, size_t* eager, size_t* captured, size_t* replayed);
+/* Fir -> QuadAmDemod fusion (on by default): a Fir with real taps whose only sink is a QuadAmDemod
+ * on the same queue is stepped with it as ONE gsdrFirFCAmDemod launch (bit-identical output).
+ * gspDriverFusedSteps counts the fused edge moves. */
+GSP_API uint32_t gspDriverSetFuseFirAm(gspHandle driver, int32_t on);
+GSP_API uint32_t gspDriverFusedSteps(gspHandle driver, size_t* fused);
 /* Name given to `node` by setupNode (this driver or a nested one); *found = 0 if none. Returns the
  * name length; at most nameBufLen bytes are written (NUL-terminated when it fits). */
 GSP_API size_t gspDriverNodeName(gspHandle driver, gspHandle node, char* name, size_t nameBufLen, int32_t* found);

@@ -178,7 +178,7 @@ def test_am_chain_odd_chunk_batches_replay(chain_mod, orc):
     multi = chain_mod.AmChain(rf, D, au, Da, L)
     base = multi.graph_captures()
     buf = torch.empty(2 * L * n, dtype=torch.int8, device="cuda")  # the live stream's input buffer
-    out = torch.empty(multi.chunks_output_count(n), dtype=torch.float32, device="cuda")
+    out = torch.empty(n * (L // (D * Da)), dtype=torch.float32, device="cuda")  # a steady batch's audio
     got = []
     for k in range(calls):
         multi.torch_stream.synchronize()  # the previous batch read buf in place
@@ -215,14 +215,16 @@ def test_am_chain_reports_ws_abort(chain_mod, orc):
     prev = ops.set_ws_spin_limit(0)
     try:
         c = chain_mod.AmChain(rf, D, au, Da, L)
-        out = torch.empty(c.resident_output_count(2), dtype=torch.float32, device="cuda")
+        out = torch.empty(4 * (L // (D * Da)), dtype=torch.float32, device="cuda")
         c.step_resident(dev, 2, out)
         c.torch_stream.synchronize()
         with pytest.raises(HipError):
             c.step_resident(dev[2 * L * 2:], 2, out)
+        taken = ops.ws_aborts(reset=True)
     finally:
         ops.set_ws_spin_limit(prev)
-    assert ops.ws_aborts(reset=True) == 0  # the failed step took the count
+        ops.ws_aborts(reset=True)  # never leak an abort into later tests
+    assert taken == 0  # the failed step took the count
     c.reset()
     base = c.graph_captures()
     n = c.step_resident(dev, 4, torch.empty(c.resident_output_count(4), dtype=torch.float32, device="cuda"))

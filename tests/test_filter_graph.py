@@ -467,7 +467,8 @@ def test_graph_replay_reports_ws_abort(graph, orc):
     finally:
         ops.set_ws_spin_limit(prev_spin)
         ops.set_kernel_policy(prev_pol)
-    ops.ws_aborts(reset=True)
+        torch.cuda.synchronize()
+        ops.ws_aborts(reset=True)  # never leak an abort into later tests
 
 
 def test_replay_skips_host_step_and_matches_eager(graph, orc):
@@ -478,7 +479,7 @@ def test_replay_skips_host_step_and_matches_eager(graph, orc):
     below an eager step's."""
     import time
     queue = graph.Queue.named("qr")
-    T, D, chunk, steps = 1023, 10, 1 << 17, 30
+    T, D, chunk, steps = 1023, 10, 131_070, 40  # chunk a multiple of D: the consumed count repeats
     taps = orc.lowpass_taps(T, 0.04)
     rng = np.random.default_rng(43)
     xs = [(rng.standard_normal(chunk) + 1j * rng.standard_normal(chunk)).astype(np.complex64) for _ in range(steps)]
@@ -505,3 +506,48 @@ def test_replay_skips_host_step_and_matches_eager(graph, orc):
     assert outs["graphed"].tobytes() == outs["eager"].tobytes()
     assert len(outs["eager"]) > 0
     assert host["graphed"] < host["eager"], host
+
+
+@pytest.mark.parametrize("elem,T,D", [("c", 1023, 10), ("c", 127, 1), ("i8", 1023, 10), ("i8", 127, 1)])
+def test_fused_fir_am_edge_matches_unfused(graph, orc, elem, T, D):
+    """The driver steps a Fir (real taps) -> QuadAmDemod edge as ONE fused launch
+    (gsdrFirFCAmDemod / gsdrInt8FirFCAmDemod): over random push sizes the stream equals the
+    reference's two-launch stepping (fusion off) bit for bit, the AM node's window stays empty, and
+    the float64 oracle chain bounds it."""
+    queue = graph.Queue.named("qu")
+    rng = np.random.default_rng(T + D + len(elem))
+    taps = orc.lowpass_taps(T, 0.4 / D)
+    et = graph.SAMPLE_FLOAT_COMPLEX if elem == "c" else graph.SAMPLE_INT8_COMPLEX
+    sizes = [int(rng.integers(1, 300_000)) for _ in range(8)]
+    if elem == "c":
+        chunks = [(rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64) for n in sizes]
+    else:
+        chunks = [rng.integers(-128, 128, size=2 * n).astype(np.int8) for n in sizes]
+    outs, stats = {}, {}
+    for fuse in (False, True):
+        fir = graph.Node.fir(queue, taps, D, et)
+        am = graph.Node.quad_am_demod(queue)
+        d2h = graph.Node.from_json("HipMemcpy", '{"commandQueue": "qu", "from": "device", "to": "host"}', queue)
+        drv = graph.SteppingDriver()
+        drv.set_fuse_fir_am(fuse)
+        drv.connect(fir, 0, am, 0)
+        drv.connect(am, 0, d2h, 0)
+        got = []
+        for c in chunks:
+            fir.push(c)
+            for _ in range(16):
+                drv.do_filter()
+                got.append(_read_host(graph, queue, d2h))
+                if fir.output_size()[0] == 0 and am.output_size()[0] == 0:
+                    break
+        outs[fuse] = np.concatenate(got)
+        stats[fuse] = drv.graph_stats()["fused"]
+        if fuse:
+            assert am.output_size()[0] == 0
+    assert stats[False] == 0 and stats[True] > 0
+    assert outs[True].tobytes() == outs[False].tobytes()
+    stream = np.concatenate(chunks)
+    x = stream if elem == "c" else orc.int8_to_float(stream).view(np.complex64)
+    y64, bound = orc.fir_f64(taps, x, D, len(outs[True]))
+    assert len(outs[True]) == (len(x) - (T - 1) - 1) // D + 1
+    assert np.all(np.abs(outs[True] - np.abs(y64)) <= FIR_TOL * bound + 1e-6 * np.abs(y64) + 1e-30)

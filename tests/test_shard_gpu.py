@@ -42,6 +42,10 @@ def _rank_main(rank, world, port, kind, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
+    # up to 8 processes time-share one GPU here, so a wave-specialised kernel's hand-off wait can be
+    # stalled far longer than on a GPU of its own: give them room, and fail loudly on any abort
+    ops.set_ws_spin_limit(1 << 28)
+    ops.ws_aborts(reset=True)
     outs = []
     if kind == "c4":
         T, D, L = 1023, 1, 20_000
@@ -76,6 +80,9 @@ def _rank_main(rank, world, port, kind, out_dir):
             out = sh.step()
             torch.cuda.synchronize()
             outs.append(out.cpu().numpy().copy())
+    aborts = ops.ws_aborts(reset=True)
+    if aborts:
+        raise RuntimeError(f"rank {rank}: {aborts} wave-specialised hand-off aborts")
     np.save(os.path.join(out_dir, f"{kind}_rank{rank}.npy"), np.stack(outs))
     dist.barrier()
     dist.destroy_process_group()
