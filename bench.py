@@ -514,6 +514,29 @@ def extra_line(wl, chain, elapsed, kernel_ms, steps, world):
             "algorithmic_bytes_per_launch": bytes_}
 
 
+def mixed_vs_plain(ops, chain, reps=10):
+    """The fused frequency shifter on the C3 kernel: gsdrMixFirFCAmDemod (mixer folded into the FFT
+    kernel: row chirp, c_p in G) against gsdrFirFCAmDemod over the same resident C3 input, HIP
+    events around `reps` launches each (interleaved twice)."""
+    x, n = chain.slot.buf, chain.geom.outputs
+    out = torch.empty(n, dtype=torch.float32, device=x.device)
+    ts = {"plain": [], "mixed": []}
+    for _ in range(2):
+        for kind in ("plain", "mixed"):
+            mix = (0.3, -2 * np.pi * 0.0731) if kind == "mixed" else None
+            ops.fir(chain.taps, x, chain.D, n, out=out, am=True, mix=mix)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(reps):
+                ops.fir(chain.taps, x, chain.D, n, out=out, am=True, mix=mix)
+            b.record()
+            b.synchronize()
+            ts[kind].append(a.elapsed_time(b) / reps)
+    plain, mixed = min(ts["plain"]), min(ts["mixed"])
+    return {"what": "C3 shape (2^28 - 6 cf32, 1023 taps, D = 10, AM): gsdrMixFirFCAmDemod vs gsdrFirFCAmDemod",
+            "plain_ms": plain, "mixed_ms": mixed, "mixed_over_plain": mixed / plain}
+
+
 def node_path(ops, device, kernel_value, segments=5, warmup=1):
     """C3 through the reference's filter-graph API (getFactoriesSingleton nodes, SteppingDriver):
     Fir(real taps, FloatComplex, D = 10) -> QuadAmDemod -> a device sink taking one C3 segment of AM
@@ -640,6 +663,8 @@ def main():
     # the C5 chain, and (N = 1) C3 through the reference's node API
     extras = {}
     if args.workload == "c3" and not args.no_extras:
+        if world == 1:
+            extras["c3_mixed"] = mixed_vs_plain(ops, chain)
         chain_info = (chain.kernel_class, kernel_name(chain), chain.L, chain.T, chain.D, chain.kind, chain.geom,
                       getattr(chain, "n_slots", 1))
         del chain

@@ -740,10 +740,14 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
   DevicePush push(device);
   if (!push.ok) return hipErrorInvalidDevice;
 
-  // long real-tap filters on cf32 / int8 IQ: FFT fast convolution (HBM-bound; fir_fft.hip)
-  if constexpr (MODE == kFirFC && (INK == kInI8IQ || INK == kInCF32) && EPI != kEpiPair && EPI != kEpiFm) if (!mix.on) {
-    if ((kernelPolicy() & (GSDR_POLICY_NO_FFT | GSDR_POLICY_NO_MFMA)) == 0 && firFftEligible(tapCount, decimation, in, INK == kInI8IQ))
-      return launchFirFft(in, INK == kInI8IQ, taps, tapCount, decimation, out, nOut, EPI, stream);
+  // long real-tap filters on cf32 / int8 IQ: FFT fast convolution (HBM-bound; fir_fft.hip), with the
+  // frequency shifter folded into it when mixing (row chirp on the loaded rows, the per-phase factor
+  // in the filter spectra, the block's factor on the outputs)
+  if constexpr (MODE == kFirFC && (INK == kInI8IQ || INK == kInCF32) && EPI != kEpiPair && EPI != kEpiFm) {
+    if ((kernelPolicy() & (GSDR_POLICY_NO_FFT | GSDR_POLICY_NO_MFMA)) == 0 &&
+        firFftEligible(tapCount, decimation, in, INK == kInI8IQ, mix.on))
+      return launchFirFft(in, INK == kInI8IQ, taps, tapCount, decimation, out, nOut, EPI, stream,
+                          FftMix{mix.on, mix.phase0, mix.step});
   }
   // int8 IQ with real taps: the exact int8 MFMA kernel when the shape allows it (the matrix-core
   // kernels take unmixed samples: a mixed stream is no longer integer)

@@ -73,7 +73,42 @@ struct Args {
   int32_t V;            // outputs per block
   float inScale;        // 1 (cf32) or 1/127 (int8 IQ): folded into G
   float guardRatio;     // direct-form fallback when max/min row-group level exceeds this
+  uint64_t mixPhase0;   // fused frequency shifter (kernels with MIX): sample n of `in` is multiplied
+  uint64_t mixStep;     // by exp(j theta(n)), theta(n) = 2 pi (mixPhase0 + n mixStep) / 2^64
 };
+
+// ---- fused frequency shifter -----------------------------------------------------------------------
+// Sample n = (b V + r) D + p of block b (row r, phase p) is multiplied by
+//     exp(j theta(n)) = E_b . T_r . c_p,   E_b = exp(j 2 pi (phase0 + b V D step) / 2^64),
+//     T_r = exp(j 2 pi r D step / 2^64),   c_p = exp(j 2 pi p step / 2^64)
+// (all phases reduced exactly in 64-bit fixed point, the exponentials in double, rounded once):
+// T_r is a per-lane table (rows l + 64 j) applied to the loaded rows - one complex multiply per
+// sample; c_p is a constant per phase, folded into G_p; E_b is a constant per block, which the
+// linear transform carries to the outputs (|E_b y| = |y|: the AM epilogue needs nothing).
+__device__ __forceinline__ f2 turnExp(uint64_t frac) {  // exp(j 2 pi frac / 2^64)
+  double sn, cs;
+  sincospi((double)(int64_t)frac * 1.0842021724855044e-19, &sn, &cs);  // 2 / 2^64
+  return f2{(float)cs, (float)sn};
+}
+// The same in float at ~2 ulp, cheap on registers (the per-block factor): the top 24 bits of the
+// phase are an exact float fraction of a turn (sincospif), the low 40 bits a rotation below
+// 2 pi 2^-24 rad, where exp(j d) = 1 - d^2 / 2 + j d to float precision.
+__device__ __forceinline__ f2 turnExpF(uint64_t frac) {
+  const int32_t hi = (int32_t)(frac >> 40) << 8 >> 8;  // signed top 24 bits: turns * 2^24
+  float sh, ch;
+  sincospif((float)hi * 1.1920928955078125e-7f, &sh, &ch);  // 2 * hi / 2^24 half-turns
+  const float d = (float)(int64_t)(frac & 0xFFFFFFFFFFull) * 3.4061215800865545e-19f;  // 2 pi / 2^64
+  const float cl = fmaf(-0.5f * d, d, 1.0f);
+  return f2{fmaf(ch, cl, -(sh * d)), fmaf(sh, cl, ch * d)};
+}
+// The VALU kernels' per-sample rotation (fir.hip mixSample): the direct-form fallback block.
+__device__ __forceinline__ f2 mixOne(const Args& a, int64_t n, f2 z) {
+  const uint64_t ph = a.mixPhase0 + (uint64_t)n * a.mixStep;
+  const float th = (float)((double)(int64_t)ph * 3.4061215800865545e-19);  // 2 pi / 2^64
+  float sn, cs;
+  sincosf(th, &sn, &cs);
+  return f2{fmaf(z.x, cs, -(z.y * sn)), fmaf(z.x, sn, z.y * cs)};
+}
 
 // ---------------------------------------------------------------- packed complex arithmetic
 // Written as VOP3P with op_sel / neg modifiers: the compiler otherwise builds the swapped /
@@ -284,14 +319,23 @@ constexpr int scratchComplex(int input) {
                         : ((1024 * D + 16) / 8 > 2 * kXch ? (1024 * D + 16 + 7) / 8 : 2 * kXch);
 }
 
-template <int D, int IN>
+constexpr int kMixT = 8 * 64;  // the row-chirp table T_r, per-lane float4 pairs like G
+
+template <int D, int IN, bool MIX = false>
 constexpr size_t ldsBytes() {
-  return (size_t)(D * 8 * 64 + kTw + kWaves * scratchComplex<D>(IN)) * sizeof(f2);
+  return (size_t)(D * 8 * 64 + kTw + kWaves * scratchComplex<D>(IN) + (MIX ? kMixT : 0)) * sizeof(f2);
 }
 
-// Prologue: the twiddle tables and G_p = inScale * conj(DFT_512(h_p)) / 512 in layout F.
-template <int D, int IN, int NW = kWaves>
-__device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l) {
+// Prologue: the twiddle tables and G_p = inScale * conj(DFT_512(h_p)) / 512 in layout F (MIX: times
+// c_p, and the row-chirp table T at mixT: f4 (T_j, T_j+1) at (j / 2) 64 + l, rows r = l + 64 j).
+template <int D, int IN, int NW = kWaves, bool MIX = false>
+__device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l, f2* mixT = nullptr) {
+  if constexpr (MIX) {
+    for (int n = threadIdx.x; n < kMixT; n += NW * kWave) {
+      const int lane = (n >> 1) & 63, j = 2 * (n >> 7) + (n & 1);
+      mixT[n] = turnExp((uint64_t)((lane + 64 * j) * D) * a.mixStep);
+    }
+  }
   for (int n = threadIdx.x; n < kTw; n += NW * kWave) {
     // complex n = ((stage 4 + kp) 64 + lane) 2 + (k & 1), k = 2 kp + (n & 1), r = k + 1
     const int stage = n >> 9, kp = (n >> 7) & 3, lane = (n >> 1) & 63, r = 2 * kp + (n & 1) + 1;
@@ -318,11 +362,34 @@ __device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l
       z[0][j] = f2{(q < a.Q && t < a.T) ? a.taps[t] : 0.0f, 0.0f};
     }
     fftFwd<1>(z, L, l);
+    if constexpr (MIX) {  // G_p c_p, the product in double and rounded once
+      double sn, cs;
+      sincospi((double)(int64_t)((uint64_t)p * a.mixStep) * 1.0842021724855044e-19, &sn, &cs);
 #pragma unroll
-    for (int d = 0; d < 8; d += 2)
-      L.g[(p * 4 + d / 2) * 64 + l] = f4{z[0][d].x * sc, -z[0][d].y * sc, z[0][d + 1].x * sc, -z[0][d + 1].y * sc};
+      for (int d = 0; d < 8; ++d) {
+        const double gr = (double)z[0][d].x * sc, gi = -(double)z[0][d].y * sc;
+        z[0][d] = f2{(float)(gr * cs - gi * sn), (float)(gr * sn + gi * cs)};
+      }
+#pragma unroll
+      for (int d = 0; d < 8; d += 2)
+        L.g[(p * 4 + d / 2) * 64 + l] = f4{z[0][d].x, z[0][d].y, z[0][d + 1].x, z[0][d + 1].y};
+    } else {
+#pragma unroll
+      for (int d = 0; d < 8; d += 2)
+        L.g[(p * 4 + d / 2) * 64 + l] = f4{z[0][d].x * sc, -z[0][d].y * sc, z[0][d + 1].x * sc, -z[0][d + 1].y * sc};
+    }
   }
   __syncthreads();
+}
+
+// This lane's row-chirp factors T_{l + 64 j}, j = 0..7.
+__device__ __forceinline__ void loadMixT(f2 (&t)[8], const f4* mixT4, int l) {
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp) {
+    const f4 v = mixT4[jp * 64 + l];
+    t[2 * jp] = f2{v.x, v.y};
+    t[2 * jp + 1] = f2{v.z, v.w};
+  }
 }
 
 // The block's rows in registers: rows[j][p] = x[(l + 64 j) D + p] (cf32), or the raw int8 IQ
@@ -472,7 +539,7 @@ __device__ __forceinline__ bool blockNeedsDirect(const Args& a, const Rows<D, IN
 }
 
 // Direct-form fallback for one block (outputs b V + m, m < V): lane l computes m = l + 64 h.
-template <int D, int IN, int EPI>
+template <int D, int IN, int EPI, bool MIX = false>
 __device__ void directBlock(const Args& a, int64_t b, int l) {
   const int64_t k0 = b * (int64_t)a.V;
   const int64_t left = a.nOut - k0;
@@ -499,6 +566,11 @@ __device__ void directBlock(const Args& a, int64_t b, int l) {
           xr = int8ToNorm(iq[0]);
           xi = int8ToNorm(iq[1]);
         }
+        if constexpr (MIX) {
+          const f2 zm = mixOne(a, base + m * D + t, f2{xr, xi});
+          xr = zm.x;
+          xi = zm.y;
+        }
         pr = fmaf(hv, xr, pr);
         pi = fmaf(hv, xi, pi);
       }
@@ -514,8 +586,11 @@ __device__ void directBlock(const Args& a, int64_t b, int l) {
 
 // The block's outputs from its rows: D forward FFTs (two phases at a time), Y = sum_p X_p G_p,
 // one inverse FFT, the first V outputs stored (AM envelope or complex).
-template <int D, int IN, int EPI>
-__device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& R, int64_t b, const Lds& L, int l) {
+// MIX with int8 rows: `t` holds this lane's row-chirp factors, applied as the points are formed
+// (cf32 rows were rotated when they landed).
+template <int D, int IN, int EPI, bool MIX = false>
+__device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& R, int64_t b, const Lds& L, int l,
+                                              const f2* t = nullptr) {
   constexpr int NP = (D % 2 == 0) ? 2 : 1;  // phases transformed together
   f2 acc[1][8];
 #pragma unroll
@@ -526,7 +601,7 @@ __device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& 
 #pragma unroll
     for (int n = 0; n < NP; ++n)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) z[n][j] = R.point(j, p + n);
+      for (int j = 0; j < 8; ++j) z[n][j] = (MIX && IN == kI8) ? cmul(R.point(j, p + n), t[j]) : R.point(j, p + n);
     fftFwd<NP>(z, L, l);
 #pragma unroll
     for (int n = 0; n < NP; ++n) {
@@ -544,6 +619,11 @@ __device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& 
     }
   }
   ifft512(acc, L, l);
+  if constexpr (MIX && EPI != kAm) {  // the block's factor E_b (|E_b y| = |y|: AM needs none)
+    const f2 eb = turnExpF(a.mixPhase0 + (uint64_t)(b * (int64_t)a.V * D) * a.mixStep);
+#pragma unroll
+    for (int h = 0; h < 8; ++h) acc[0][h] = cmul(acc[0][h], eb);
+  }
   // outputs k0 + m, m < nv: the bound and the base are wave-uniform, so the lane math stays
   // 32-bit (per-lane 64-bit output indices were spilled to scratch, and each reload between the
   // stores waited for the stores before it: s_waitcnt vmcnt(0))
@@ -562,16 +642,17 @@ __device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& 
   }
 }
 
-template <int D, int IN, int EPI>
+template <int D, int IN, int EPI, bool MIX = false>
 __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) f2 lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   f2* twAll = lds + D * 8 * 64;
+  f2* mixT = twAll + kTw + kWaves * scratchComplex<D>(IN);
   Lds L;
   L.g = reinterpret_cast<f4*>(lds);
   L.tw = reinterpret_cast<const f4*>(twAll) + l;
   L.scratch = twAll + kTw + w * scratchComplex<D>(IN);
-  buildTables<D, IN>(a, twAll, L, w, l);
+  buildTables<D, IN, kWaves, MIX>(a, twAll, L, w, l, mixT);
 
   // round r: workgroup g's wave w takes block (r * groups + g) * kWaves + w, so in every round
   // the grid streams one contiguous stretch of the input (DRAM-friendly, like a grid-stride copy)
@@ -580,9 +661,19 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   for (int64_t b = (int64_t)blockIdx.x * kWaves + w; b < a.nBlocks; b += stride) {
     Rows<D, IN> R;
     loadRows<D>(a, b, R, L.scratch, l);
+    f2 t[8];
+    if constexpr (MIX) {  // the row chirp: cf32 rows rotated here, int8 rows as they become points
+      loadMixT(t, reinterpret_cast<const f4*>(mixT), l);
+      if constexpr (IN == kCf32) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int p = 0; p < D; ++p) R.v[j][p] = cmul(R.v[j][p], t[j]);
+      }
+    }
     if (blockNeedsDirect<D, IN>(a, R, b, l)) {
       if (l == 0) atomicAdd(&gDirectBlocks, 1ull);
-      directBlock<D, IN, EPI>(a, b, l);
+      directBlock<D, IN, EPI, MIX>(a, b, l);
       continue;
     }
     // The two waves of a SIMD overlap one's loads with the other's FFTs only while they are out
@@ -592,7 +683,7 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
     // This replaces the start-up stagger (s_sleep for half the waves) of earlier builds, which
     // is neutral on top of it.
     __builtin_amdgcn_s_setprio(2);
-    convolveBlock<D, IN, EPI>(a, R, b, L, l);
+    convolveBlock<D, IN, EPI, MIX>(a, R, b, L, l, t);
     __builtin_amdgcn_s_setprio(0);
   }
 }
@@ -809,11 +900,11 @@ int cuCount() {
   return n;
 }
 
-template <int D, int IN, int EPI>
+template <int D, int IN, int EPI, bool MIX>
 hipError_t launchD(fftfir::Args a, hipStream_t stream) {
   using namespace fftfir;
-  auto kernel = firFftKernel<D, IN, EPI>;
-  const size_t lds = ldsBytes<D, IN>();
+  auto kernel = firFftKernel<D, IN, EPI, MIX>;
+  const size_t lds = ldsBytes<D, IN, MIX>();
   // set per launch (cheap): a once-per-process flag would race between threads and miss other devices
   const hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -839,14 +930,14 @@ hipError_t launchD1(fftfir::Args a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-template <int IN, int EPI>
+template <int IN, int EPI, bool MIX = false>
 hipError_t launchFft(fftfir::Args a, size_t D, hipStream_t stream) {
   switch (D) {
-    case 2: return launchD<2, IN, EPI>(a, stream);
-    case 4: return launchD<4, IN, EPI>(a, stream);
-    case 6: return launchD<6, IN, EPI>(a, stream);
-    case 8: return launchD<8, IN, EPI>(a, stream);
-    case 10: return launchD<10, IN, EPI>(a, stream);
+    case 2: return launchD<2, IN, EPI, MIX>(a, stream);
+    case 4: return launchD<4, IN, EPI, MIX>(a, stream);
+    case 6: return launchD<6, IN, EPI, MIX>(a, stream);
+    case 8: return launchD<8, IN, EPI, MIX>(a, stream);
+    case 10: return launchD<10, IN, EPI, MIX>(a, stream);
     default: return hipErrorInvalidValue;
   }
 }
@@ -855,9 +946,10 @@ hipError_t launchFft(fftfir::Args a, size_t D, hipStream_t stream) {
 
 // Eligible: real taps (FC), D in {2,4,6,8,10}, enough taps that the FFT beats the direct forms,
 // at least 64 outputs per block, and the loads' alignment (cf32: 16-byte input; int8 IQ: 4-byte).
-bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int8Iq) {
+bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int8Iq, bool mixed) {
   const size_t D = decimation < 1 ? 1 : decimation;
   if (D == 1) {  // cf32: eight output phases per block (firFftD1PfKernel), up to 3 584 taps
+    if (mixed) return false;
     const size_t Q = (tapCount + 7) / 8;
     return !int8Iq && tapCount >= 256 && Q <= (size_t)fftfir::kM - 64 && ((uintptr_t)in & 15) == 0;
   }
@@ -868,18 +960,18 @@ bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int
   // int8 IQ: the exact f16 MFMA kernels are faster where they apply (C5 RF stage, 125 M samples:
   // 195 us wave-specialised MFMA vs 263 us FFT); the FFT takes the shapes they cannot
   if (int8Iq)
-    return (p & 3) == 0 && ((kernelPolicy() & GSDR_POLICY_PREFER_FFT) != 0 ||
+    return (p & 3) == 0 && (mixed || (kernelPolicy() & GSDR_POLICY_PREFER_FFT) != 0 ||
                             (!firI8MfmaEligible(tapCount, decimation, in) && !firI8DecMfmaEligible(tapCount, decimation, in)));
   return (p & 15) == 0;
 }
 
 hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t tapCount, size_t decimation,
-                        void* out, size_t nOut, int epi, hipStream_t stream) {
+                        void* out, size_t nOut, int epi, hipStream_t stream, FftMix mix) {
   using namespace fftfir;
   if (nOut == 0) return hipSuccess;
   const size_t D = decimation < 1 ? 1 : decimation;
   if (D == 1) {
-    if (int8Iq) return hipErrorInvalidValue;
+    if (int8Iq || mix.on) return hipErrorInvalidValue;
     Args a{};
     a.in = in;
     a.taps = taps;
@@ -909,6 +1001,12 @@ hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t t
   a.inScale = int8Iq ? 1.0f / 127.0f : 1.0f;
   a.guardRatio = gFftGuard.load(std::memory_order_relaxed);
   const bool am = epi == kEpiAm;
+  if (mix.on) {
+    a.mixPhase0 = mix.phase0;
+    a.mixStep = mix.step;
+    if (int8Iq) return am ? launchFft<kI8, kAm, true>(a, D, stream) : launchFft<kI8, kComplex, true>(a, D, stream);
+    return am ? launchFft<kCf32, kAm, true>(a, D, stream) : launchFft<kCf32, kComplex, true>(a, D, stream);
+  }
   if (int8Iq) return am ? launchFft<kI8, kAm>(a, D, stream) : launchFft<kI8, kComplex>(a, D, stream);
   return am ? launchFft<kCf32, kAm>(a, D, stream) : launchFft<kCf32, kComplex>(a, D, stream);
 }

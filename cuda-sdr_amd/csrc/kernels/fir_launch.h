@@ -49,9 +49,15 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
 
 // cf32 (16-byte aligned) or int8 IQ (4-byte aligned) x real taps, long filters, D in {2,4,6,8,10}:
 // polyphase overlap-save FFT fast convolution (fir_fft.hip).
-bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int8Iq);
+// mixed: the fused frequency shifter (gsdr*MixFirFC*) - D >= 2 only, and for int8 IQ the FFT is then
+// the long-filter kernel (the int8 MFMA kernels need unmixed integer samples).
+struct FftMix {
+  bool on = false;
+  uint64_t phase0 = 0, step = 0;  // theta(n) = 2 pi (phase0 + n step) / 2^64
+};
+bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int8Iq, bool mixed = false);
 hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t tapCount, size_t decimation,
-                        void* out, size_t nOut, int epi, hipStream_t stream);
+                        void* out, size_t nOut, int epi, hipStream_t stream, FftMix mix = FftMix{});
 
 // Kernel-selection policy bits (gsdrAmdSetKernelPolicy).
 uint32_t kernelPolicy();

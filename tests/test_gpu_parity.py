@@ -608,7 +608,12 @@ def test_quad_fm_demod_kernel(ops, orc):
 
 
 @pytest.mark.parametrize("kind,T,D,n_out", [("c64", 127, 1, 5000), ("c64", 1023, 10, 3000), ("i8", 127, 1, 70000),
-                                             ("i8", 1023, 10, 20000), ("c64", 64, 3, 1), ("i8", 255, 4, 777)])
+                                             ("i8", 1023, 10, 20000), ("c64", 64, 3, 1), ("i8", 255, 4, 777),
+                                             # FFT kernel shapes (T >= 256, D in 2..10): the row chirp /
+                                             # c_p-in-G / per-block factor decomposition
+                                             ("c64", 1023, 10, 200_000), ("c64", 1023, 4, 60_000),
+                                             ("c64", 300, 2, 50_001), ("i8", 1023, 10, 150_000),
+                                             ("i8", 511, 6, 40_000)])
 def test_fused_frequency_shift_fir(ops, orc, kind, T, D, n_out):
     """Frequency shifter fused into the FIR load (gsdr*MixFirFC*): against the oracle mixer
     (exact 64-bit phase, float32 angle, float64 exponential) and float64 FIR; the AM variant
@@ -724,3 +729,38 @@ def test_zero_length_calls_are_no_ops(ops):
     assert L.gsdrCosineF(ctypes.c_float(0.0), ctypes.c_float(1.0), None, 0, 0, stream) == 0
     torch.cuda.synchronize()
     assert torch.all(sentinel == 7.0)
+
+
+@pytest.mark.parametrize("kind", ["c64", "i8"])
+def test_mixed_long_filter_runs_on_fft_kernel(ops, orc, kind):
+    """A mixed long filter (gsdrMixFirFC*, 1023 taps, D = 10) takes the FFT kernel (it
+    fell back to the VALU direct form): with the accuracy guard forced to 0 every FFT block goes to
+    the kernel's direct-form fallback, which the block counter shows; that fallback (per-sample
+    rotation) and the FFT path (decomposed rotation) both meet the float64 oracle, AM and complex."""
+    T, D, n_out = 1023, 10, 60_000
+    n_in = (n_out - 1) * D + T
+    rng = np.random.default_rng(77)
+    phase0, step = -0.7, 2 * np.pi * 0.0123
+    taps = orc.lowpass_taps(T, 0.04)
+    if kind == "c64":
+        x = (rng.standard_normal(n_in) + 1j * rng.standard_normal(n_in)).astype(np.complex64)
+        xd, xf = _dev(x), x
+    else:
+        iq = rng.integers(-128, 128, size=2 * n_in).astype(np.int8)
+        xd, xf = _dev(iq), orc.int8_to_float(iq).view(np.complex64)
+    td = _dev(taps)
+    y64, bound = orc.fir_f64(taps, orc.mix_f64(xf, phase0, step).astype(np.complex64), D, n_out)
+    ops.fft_direct_blocks(reset=True)
+    prev = ops.set_fft_guard(0.0)
+    try:
+        y_dir = _host(ops.fir(td, xd, D, n_out, int8_iq=(kind == "i8"), mix=(phase0, step)))
+        am_dir = _host(ops.fir(td, xd, D, n_out, int8_iq=(kind == "i8"), am=True, mix=(phase0, step)))
+        assert ops.fft_direct_blocks(reset=True) > 0  # the FFT kernel ran (all its blocks direct)
+    finally:
+        ops.set_fft_guard(prev)
+    y = _host(ops.fir(td, xd, D, n_out, int8_iq=(kind == "i8"), mix=(phase0, step)))
+    am = _host(ops.fir(td, xd, D, n_out, int8_iq=(kind == "i8"), am=True, mix=(phase0, step)))
+    assert ops.fft_direct_blocks(reset=True) == 0
+    for yy, aa, what in ((y, am, "fft"), (y_dir, am_dir, "direct")):
+        _check_fir(yy, y64, bound, ("mixed", kind, what))
+        assert np.all(np.abs(aa - np.abs(y64)) <= FIR_TOL * bound + 1e-30), what
