@@ -819,19 +819,29 @@ __device__ __forceinline__ void convolveBlockD1(const Args& a, const Rows<8, kCf
         g[d + 1] = f2{v.z, v.w};
       }
       const int t = p + r;
+      // the two halves of the eight complex MACs issued stage-interleaved: a v_pk_fma right
+      // behind the one that writes its operand costs an s_nop (one wave per SIMD: nothing hides it)
+      f2 u[8];
+#pragma unroll
+      for (int d = 0; d < 8; ++d) u[d] = t < D ? cmac1(X[t][d], g[d], acc[0][d]) : cmac1(X[t - D][d], g[d], sh[d]);
 #pragma unroll
       for (int d = 0; d < 8; ++d) {
-        if (t < D) acc[0][d] = cmac(X[t][d], g[d], acc[0][d]);
-        else sh[d] = cmac(X[t - D][d], g[d], sh[d]);
+        if (t < D) acc[0][d] = cmul2(X[t][d], g[d], u[d]);
+        else sh[d] = cmul2(X[t - D][d], g[d], u[d]);
       }
     }
     if (r > 0) {  // the one-row advance of the wrapped phases
+      f2 om[8], u[8];
 #pragma unroll
       for (int d = 0; d < 8; d += 2) {
         const f4 v = omega[(d / 2) * 64];
-        acc[0][d] = cmac(sh[d], f2{v.x, v.y}, acc[0][d]);
-        acc[0][d + 1] = cmac(sh[d + 1], f2{v.z, v.w}, acc[0][d + 1]);
+        om[d] = f2{v.x, v.y};
+        om[d + 1] = f2{v.z, v.w};
       }
+#pragma unroll
+      for (int d = 0; d < 8; ++d) u[d] = cmac1(sh[d], om[d], acc[0][d]);
+#pragma unroll
+      for (int d = 0; d < 8; ++d) acc[0][d] = cmul2(sh[d], om[d], u[d]);
     }
     ifft512(acc, L, l);
     // outputs 8 (row0 + m) + r for m < nv (wave-uniform bound and base, 32-bit lane math)

@@ -12,7 +12,13 @@
 
 #define DECL(N)                                                                                        \
   namespace f##N {                                                                                     \
-  hipError_t launchFirFft(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t); \
+  struct FftMix {                                                                                      \
+    bool on = false;                                                                                   \
+    uint64_t phase0 = 0, step = 0;                                                                     \
+  };                                                                                                   \
+  hipError_t launchFirFft(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t, FftMix); \
+  inline hipError_t launchPlain(const void* i, bool b, const float* t, size_t T, size_t D, void* o, size_t n, int e, \
+                                hipStream_t s) { return launchFirFft(i, b, t, T, D, o, n, e, s, FftMix{}); } \
   uint32_t kernelPolicy() { return 0; }                                                              \
   bool firI8MfmaEligible(size_t, size_t, const void*) { return false; }                              \
   bool firI8DecMfmaEligible(size_t, size_t, const void*) { return false; }                           \

@@ -30,7 +30,7 @@ if [ "${1:-build}" = build ]; then
     hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Iinclude -Icuda-sdr_amd/csrc/kernels \
       -Dgsdr_amd=f$i -DgsdrAmdSetFftGuard=f${i}_sg -DgsdrAmdGetFftGuard=f${i}_gg -DgsdrAmdFftDirectBlocks=f${i}_db \
       $flags -c ${src:-$ASRC} -o $OUT/f$i.o &
-    decls="$decls DECL($i)"; table="$table {\"$name\", f$i::launchFirFft},"; objs="$objs $OUT/f$i.o"
+    decls="$decls DECL($i)"; table="$table {\"$name\", f$i::launchPlain},"; objs="$objs $OUT/f$i.o"
     i=$((i+1))
   done <<< "$VARIANTS"
   wait
