@@ -1607,6 +1607,17 @@ uint32_t* wsAbortWord(int dev) {
   return gAbortDev[dev];
 }
 
+// Aborts counted on `dev` so far, without clearing them (a host read of the mapped word).
+uint32_t peekWsAborts(int dev) {
+  if (dev < 0 || dev >= kMaxDevices) return 0;
+  uint32_t* h;
+  {
+    std::lock_guard<std::mutex> lock(gAbortMu);
+    h = gAbortHost[dev];
+  }
+  return h == nullptr ? 0u : __atomic_load_n(h, __ATOMIC_SEQ_CST);
+}
+
 // Aborts counted since the last read on `dev` (host read of the mapped word; clears it).
 uint32_t takeWsAborts(int dev) {
   if (dev < 0 || dev >= kMaxDevices) return 0;
@@ -1618,51 +1629,25 @@ uint32_t takeWsAborts(int dev) {
   return h == nullptr ? 0u : __atomic_exchange_n(h, 0u, __ATOMIC_SEQ_CST);
 }
 
-// Completion marker of the last eager (not captured) wave-specialised launch per device.
-hipEvent_t gLastWs[kMaxDevices];
-
 // Before a wave-specialised launch: report an earlier launch's abort, and arm this one. The abort
-// word is read only once the device's last eager WS launch has completed (its event has fired:
-// after any synchronisation the caller makes, deterministically), never while that kernel may
-// still be writing it; an abort not yet settled is reported by a later call. Under stream capture
-// nothing is read (a graph executor checks after its replays, gsdrAmdWsTakeAborts).
+// word is only peeked at (a host read); when it is set, the device is synchronised first, so the
+// count is complete and no kernel is still writing it, then it is taken: a caller that
+// synchronises after a launch gets the report from its next call, deterministically, and the
+// common case (no abort) costs no API call. Under stream capture nothing is read (a graph
+// executor checks before its next replay, gsdrAmdWsAbortsPending / gsdrAmdWsTakeAborts).
 hipError_t wsPrepare(hipStream_t stream, int32_t& spinLimit, uint32_t*& abortOut) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if ((e = hipStreamIsCapturing(stream, &cs)) != hipSuccess) return e;
-  if (cs == hipStreamCaptureStatusNone && dev >= 0 && dev < kMaxDevices) {
-    hipEvent_t ev;
-    {
-      std::lock_guard<std::mutex> lock(gAbortMu);
-      ev = gLastWs[dev];
-    }
-    const hipError_t q = ev == nullptr ? hipSuccess : hipEventQuery(ev);
-    if (q != hipSuccess && q != hipErrorNotReady) return q;
-    if (q == hipSuccess && takeWsAborts(dev) != 0) return hipErrorLaunchTimeOut;
+  if (cs == hipStreamCaptureStatusNone && peekWsAborts(dev) != 0) {
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+    if (takeWsAborts(dev) != 0) return hipErrorLaunchTimeOut;
   }
   spinLimit = gWsSpinLimit.load(std::memory_order_relaxed);
   abortOut = wsAbortWord(dev);
   return hipSuccess;
-}
-
-// After an eager wave-specialised launch on `stream`: mark its completion for wsPrepare.
-hipError_t wsLaunched(hipStream_t stream, hipError_t launch) {
-  if (launch != hipSuccess) return launch;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess || dev < 0 || dev >= kMaxDevices) return e;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if ((e = hipStreamIsCapturing(stream, &cs)) != hipSuccess || cs != hipStreamCaptureStatusNone) return e;
-  hipEvent_t ev;
-  {
-    std::lock_guard<std::mutex> lock(gAbortMu);
-    if (gLastWs[dev] == nullptr && (e = hipEventCreateWithFlags(&gLastWs[dev], hipEventDisableTiming)) != hipSuccess)
-      return e;
-    ev = gLastWs[dev];
-  }
-  return hipEventRecord(ev, stream);
 }
 
 }  // namespace
@@ -1722,7 +1707,7 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
       if (!a.dbp) lds -= kCfPartialBytes;
       if (lds <= (size_t)kCfDynLdsMax) {
         if (hipError_t e = wsPrepare(stream, a.spinLimit, a.abortOut); e != hipSuccess) return e;
-        return wsLaunched(stream, launchCfWsAny(a, Wl, lds, grid, epi, stream));
+        return launchCfWsAny(a, Wl, lds, grid, epi, stream);
       }
     }
   }
@@ -1808,7 +1793,7 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
       if (!a.dbp) lds -= kCfPartialBytes;
       if (lds <= (size_t)kCfDynLdsMax) {
         if (hipError_t e = wsPrepare(stream, a.spinLimit, a.abortOut); e != hipSuccess) return e;
-        return wsLaunched(stream, launchI8WsAny(a, Wl, lds, grid, epi, stream));
+        return launchI8WsAny(a, Wl, lds, grid, epi, stream);
       }
     }
   }
@@ -1854,6 +1839,7 @@ int32_t gsdrAmdGetWsSpinLimit(void) { return gsdr_amd::gWsSpinLimit.load(std::me
 // Graph executors (am_chain, the stepping driver): aborts counted on `device` so far, cleared; no
 // synchronisation - call it once the replays of interest are known to have completed.
 uint32_t gsdrAmdWsTakeAborts(int32_t device) { return gsdr_amd::takeWsAborts(device); }
+uint32_t gsdrAmdWsAbortsPending(int32_t device) { return gsdr_amd::peekWsAborts(device); }
 
 hipError_t gsdrAmdWsAborts(int32_t device, uint64_t* count, int reset) {
   int prev = 0;

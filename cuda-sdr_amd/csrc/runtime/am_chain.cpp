@@ -81,8 +81,6 @@ struct gsdrAmChainImpl {
   float* multiOut = nullptr;
   size_t multiChunks = 0;
   size_t captures = 0;  // graphs instantiated (creation's three + every recapture; diagnostics)
-  hipEvent_t launched = nullptr;  // after the last step's launch: its completion settles WS aborts
-  bool launchedOnce = false;
   // process-wide kernel settings baked into the cached graphs (kernel policy, FFT guard, WS spin
   // limit) at their capture
   uint64_t settings = 0;
@@ -117,10 +115,10 @@ struct gsdrAmChainImpl {
   // Step entry: fail if the previous step's launch completed with a WS abort; recapture the
   // cached graphs when a process-wide kernel setting changed since their capture.
   hipError_t enter() {
-    if (launchedOnce) {
-      const hipError_t q = hipEventQuery(launched);
-      if (q != hipSuccess && q != hipErrorNotReady) return q;
-      if (q == hipSuccess && gsdrAmdWsTakeAborts(device) != 0) return hipErrorLaunchTimeOut;
+    if (gsdrAmdWsAbortsPending(device) != 0) {  // rare: settle the count, then report it
+      AMC_TRY(hipStreamSynchronize(copyStream));
+      AMC_TRY(hipStreamSynchronize(stream));
+      if (gsdrAmdWsTakeAborts(device) != 0) return hipErrorLaunchTimeOut;
     }
     const uint64_t now = currentSettings();
     if (now != settings) {
@@ -137,10 +135,6 @@ struct gsdrAmChainImpl {
       AMC_TRY(capture(&steady[1], false, 1));
     }
     return hipSuccess;
-  }
-  hipError_t markLaunched() {
-    launchedOnce = true;
-    return hipEventRecord(launched, stream);
   }
 
   void dropMulti() {
@@ -224,7 +218,6 @@ struct gsdrAmChainImpl {
       if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : copyDone)
       if (ev) (void)hipEventDestroy(ev);
-    if (launched) (void)hipEventDestroy(launched);
     for (hipEvent_t ev : slotDone)
       if (ev) (void)hipEventDestroy(ev);
     (void)hipFree(taps);
@@ -270,7 +263,6 @@ hipError_t build(gsdrAmChainImpl* c, const gsdrAmChainConfig& cfg) {
   AMC_TRY(hipMalloc(&c->audio, sizeof(float) * (c->na1 > c->naSteady ? c->na1 : c->naSteady)));
   for (auto& ev : c->readDone) AMC_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (auto& ev : c->copyDone) AMC_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  AMC_TRY(hipEventCreateWithFlags(&c->launched, hipEventDisableTiming));
   c->settings = gsdrAmChainImpl::currentSettings();
   if (c->slots > 0) {
     AMC_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hostIn), 2 * c->L * c->slots, hipHostMallocDefault));
@@ -353,7 +345,6 @@ hipError_t gsdrAmChainStep(gsdrAmChain c, const int8_t* inputIq, float* output, 
   const size_t n = c->nextOutputs();
   AMC_TRY(hipMemcpyAsync(c->staging[p] + 2 * c->r, inputIq, 2 * c->L, hipMemcpyDeviceToDevice, c->stream));
   AMC_TRY(hipGraphLaunch(c->graphFor(p), c->stream));
-  AMC_TRY(c->markLaunched());
   AMC_TRY(hipEventRecord(c->readDone[p], c->stream));
   AMC_TRY(hipMemcpyAsync(output, c->audio, sizeof(float) * n, hipMemcpyDeviceToDevice, c->stream));
   ++c->steps;
@@ -403,7 +394,6 @@ hipError_t gsdrAmChainStepChunks(gsdrAmChain c, const int8_t* inputIq, size_t nC
     ++c->captures;
   }
   AMC_TRY(hipGraphLaunch(c->multi[key], c->stream));
-  AMC_TRY(c->markLaunched());
   // both staging parities were last read by this launch
   AMC_TRY(hipEventRecord(c->readDone[0], c->stream));
   AMC_TRY(hipEventRecord(c->readDone[1], c->stream));
@@ -434,7 +424,6 @@ hipError_t gsdrAmChainStepHost(gsdrAmChain c, size_t slot, size_t* outputCount) 
   AMC_TRY(hipEventRecord(c->copyDone[p], c->copyStream));
   AMC_TRY(hipStreamWaitEvent(c->stream, c->copyDone[p], 0));
   AMC_TRY(hipGraphLaunch(c->graphFor(p), c->stream));
-  AMC_TRY(c->markLaunched());
   AMC_TRY(hipEventRecord(c->readDone[p], c->stream));
   AMC_TRY(hipMemcpyAsync(c->hostOut + c->naSteady * slot, c->audio, sizeof(float) * n, hipMemcpyDeviceToHost,
                          c->stream));
@@ -490,7 +479,6 @@ hipError_t gsdrAmChainStepResident(gsdrAmChain c, const int8_t* inputIq, size_t 
   }
   const size_t n = c->residentAudio(nChunks);
   AMC_TRY(hipGraphLaunch(c->resident, c->stream));
-  AMC_TRY(c->markLaunched());
   // the AM history now sits at the front of amBig; the per-chunk window `am` is stale, so a later
   // per-chunk step would need a reset (documented in gsdr_amd.h)
   c->steps += nChunks;

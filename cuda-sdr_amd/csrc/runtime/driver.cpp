@@ -53,6 +53,7 @@ Status SteppingDriver::connect(Source* source, size_t sourcePort, Sink* sink, si
     SinkInfo& ki = sinkInfo(sink);
     if (ki.inputs.size() <= sinkPort) ki.inputs.resize(sinkPort + 1);
     ki.inputs[sinkPort] = Upstream{source, sourcePort};
+    mStepNodesValid = false;
 
     if (Sink* s = source->asSink()) mTails.erase(std::remove(mTails.begin(), mTails.end(), s), mTails.end());
     Source* sinkAsSource = sink->asSource();
@@ -334,11 +335,31 @@ Status SteppingDriver::doSourceOutput(Source* source, Fir* fusedFir) {
 
 SteppingDriver::~SteppingDriver() {
   for (const CachedGraph& g : mGraphs) (void)hipGraphExecDestroy(g.exec);
-  if (mGraphDone != nullptr) (void)hipEventDestroy(mGraphDone);
 }
 
-bool SteppingDriver::chainState(hipStream_t stream, uint64_t& key, std::vector<IGraphStepState*>* nodesOut) const
-    noexcept {
+bool SteppingDriver::chainState(hipStream_t stream, uint64_t& key) noexcept {
+  if (!mStepNodesValid) {  // every connected node, in a fixed order (by address)
+    mStepNodes.clear();
+    mStepNodesOk = false;
+    mStepNodesValid = true;
+    try {
+      std::vector<Node*> nodes;
+      for (Source* so : mSourceOrder) nodes.push_back(so);
+      for (const auto& kv : mSinks) nodes.push_back(kv.first);
+      std::sort(nodes.begin(), nodes.end());
+      nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
+      for (Node* n : nodes) {
+        auto* g = dynamic_cast<IGraphStepState*>(n);
+        if (g == nullptr) return false;
+        mStepNodes.push_back(g);
+      }
+    } catch (...) {
+      mStepNodes.clear();
+      return false;
+    }
+    mStepNodesOk = !mStepNodes.empty();
+  }
+  if (!mStepNodesOk) return false;
   // process-wide kernel settings that become captured launch arguments: a replay must not run with
   // values that changed since its capture (kernel policy, FFT guard ratio, WS spin limit)
   const float guard = gsdrAmdGetFftGuard();
@@ -347,19 +368,9 @@ bool SteppingDriver::chainState(hipStream_t stream, uint64_t& key, std::vector<I
   uint64_t h = 0xCBF29CE484222325ull ^ (uint64_t)gsdrAmdGetKernelPolicy();
   h = (h ^ guardBits) * 0x100000001B3ull;
   h = (h ^ (uint32_t)gsdrAmdGetWsSpinLimit()) * 0x100000001B3ull;
-  // every connected node (a fixed order: by address)
-  std::vector<Node*> nodes;
-  for (Source* so : mSourceOrder) nodes.push_back(so);
-  for (const auto& kv : mSinks) nodes.push_back(kv.first);
-  std::sort(nodes.begin(), nodes.end());
-  nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
-  if (nodes.empty()) return false;
-  if (nodesOut != nullptr) nodesOut->clear();
-  for (Node* n : nodes) {
-    auto* g = dynamic_cast<IGraphStepState*>(n);
-    if (g == nullptr || g->graphStream() != stream || !g->graphState(h)) return false;
-    h = (h ^ reinterpret_cast<uintptr_t>(n)) * 0x100000001B3ull;
-    if (nodesOut != nullptr) nodesOut->push_back(g);
+  for (IGraphStepState* g : mStepNodes) {
+    if (g->graphStream() != stream || !g->graphState(h)) return false;
+    h = (h ^ reinterpret_cast<uintptr_t>(g)) * 0x100000001B3ull;
   }
   key = h;
   return true;
@@ -379,37 +390,29 @@ Status SteppingDriver::captureStep(hipStream_t stream, hipGraph_t* graphOut) noe
   return Status_Success;
 }
 
-Status SteppingDriver::launchGraph(hipGraphExec_t exec, hipStream_t stream) noexcept {
-  SAFE_HIP_OR_RET_STATUS(hipGraphLaunch(exec, stream));
-  if (mGraphDone == nullptr) SAFE_HIP_OR_RET_STATUS(hipEventCreateWithFlags(&mGraphDone, hipEventDisableTiming));
-  SAFE_HIP_OR_RET_STATUS(hipEventRecord(mGraphDone, stream));
-  mGraphLaunched = true;
-  return Status_Success;
-}
-
 Status SteppingDriver::doFilterGraphed(hipStream_t stream) noexcept {
   try {
-    // a wave-specialised kernel inside an earlier replay that gave up a hand-off wait: reported
-    // once that replay has completed (the eager entry points cannot see graph launches)
-    if (mGraphLaunched) {
-      const hipError_t q = hipEventQuery(mGraphDone);
-      if (q != hipSuccess && q != hipErrorNotReady) SAFE_HIP_OR_RET_STATUS(q);
+    // a wave-specialised kernel inside an earlier replay that gave up a hand-off wait (the eager
+    // entry points never see graph launches): a host peek; when set, settle and report it
+    if (!mGraphs.empty()) {
       int dev = 0;
-      if (q == hipSuccess && hipStreamGetDevice(stream, &dev) == hipSuccess && gsdrAmdWsTakeAborts(dev) != 0) {
-        gsloge("SteppingDriver: a wave-specialised kernel in a replayed step aborted (hand-off wait timed out)");
-        return Status_RuntimeError;
+      if (hipStreamGetDevice(stream, &dev) == hipSuccess && gsdrAmdWsAbortsPending(dev) != 0) {
+        SAFE_HIP_OR_RET_STATUS(hipStreamSynchronize(stream));
+        if (gsdrAmdWsTakeAborts(dev) != 0) {
+          gsloge("SteppingDriver: a wave-specialised kernel in a replayed step aborted (hand-off wait timed out)");
+          return Status_RuntimeError;
+        }
       }
     }
     uint64_t key = 0;
-    std::vector<IGraphStepState*> nodes;
-    if (mGraphOff || stream == nullptr || !chainState(stream, key, &nodes)) {
+    if (mGraphOff || stream == nullptr || !chainState(stream, key)) {
       ++mStats.eager;
       return doFilter();
     }
     for (const CachedGraph& g : mGraphs) {
       if (g.key != key) continue;
       for (const auto& [node, state] : g.post) FWD_IF_ERR(node->restoreStepState(state));
-      FWD_IF_ERR(launchGraph(g.exec, stream));
+      SAFE_HIP_OR_RET_STATUS(hipGraphLaunch(g.exec, stream));
       ++mStats.replayed;
       mGraphMisses = 0;
       return Status_Success;
@@ -437,12 +440,13 @@ Status SteppingDriver::doFilterGraphed(hipStream_t stream) noexcept {
     SAFE_HIP_OR_RET_STATUS(ie);
     CachedGraph cg{key, exec, {}};
     bool saved = true;
-    cg.post.reserve(nodes.size());
-    for (IGraphStepState* n : nodes) {
+    cg.post.reserve(mStepNodes.size());
+    for (IGraphStepState* n : mStepNodes) {
       cg.post.emplace_back(n, GraphNodeState{});
       saved = saved && n->saveStepState(cg.post.back().second);
     }
-    const Status ls = launchGraph(exec, stream);
+    const hipError_t le = hipGraphLaunch(exec, stream);
+    const Status ls = le == hipSuccess ? Status_Success : Status_RuntimeError;
     if (saved && ls == Status_Success) {
       mGraphs.push_back(std::move(cg));
     } else {

@@ -122,12 +122,13 @@ class SteppingDriver final : public ISteppingDriver {
   size_t mGraphMisses = 0;
   bool mGraphOff = false;
   GraphStats mStats;
-  hipEvent_t mGraphDone = nullptr;  // after the last graph launch: wave-specialised aborts settle
-  bool mGraphLaunched = false;
+  // graph-steppable nodes in a fixed order (by address), rebuilt when a connection changes
+  std::vector<IGraphStepState*> mStepNodes;
+  bool mStepNodesValid = false;
+  bool mStepNodesOk = false;
   bool mFuseFirAm = true;
-  bool chainState(hipStream_t stream, uint64_t& key, std::vector<IGraphStepState*>* nodesOut) const noexcept;
+  bool chainState(hipStream_t stream, uint64_t& key) noexcept;
   Status captureStep(hipStream_t stream, hipGraph_t* graphOut) noexcept;
-  Status launchGraph(hipGraphExec_t exec, hipStream_t stream) noexcept;
 
   ~SteppingDriver() final;
   REF_COUNTED_NO_DESTRUCTOR(SteppingDriver);

@@ -150,11 +150,12 @@ GSDR_API hipError_t gsdrAmdFftDirectBlocks(int32_t device, uint64_t* count, int 
 GSDR_API void gsdrAmdSetWsSpinLimit(int32_t iterations);
 GSDR_API int32_t gsdrAmdGetWsSpinLimit(void);
 GSDR_API hipError_t gsdrAmdWsAborts(int32_t device, uint64_t* count, int reset);
-/* The same count, read and cleared WITHOUT synchronising: for graph executors, which call it once
- * the replays they launched are known to have completed (an event they recorded has fired). The
- * eager entry points read it only after the device's last eager WS launch has completed, so which
- * call reports an abort depends only on the caller's synchronisation, not on timing. */
+/* The same count WITHOUT synchronising: Pending peeks (no clear), Take reads and clears. For graph
+ * executors: when Pending is nonzero they synchronise their stream, then Take, then fail the step.
+ * The eager entry points do the same (device-wide), so a caller that synchronises after a launch
+ * gets an abort reported by its next call, and the common case costs no API call. */
 GSDR_API uint32_t gsdrAmdWsTakeAborts(int32_t device);
+GSDR_API uint32_t gsdrAmdWsAbortsPending(int32_t device);
 
 GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
                                     uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,
@@ -230,8 +231,8 @@ GSDR_API hipError_t gsdrAmChainWaitSlot(gsdrAmChain chain, size_t slot);
 GSDR_API size_t gsdrAmChainResidentOutputCount(gsdrAmChain chain, size_t nChunks);
 GSDR_API hipError_t gsdrAmChainStepResident(gsdrAmChain chain, const int8_t* inputIq, size_t nChunks, float* output,
                                             size_t* outputCount);
-/* Every step entry first checks the previous step's launch: once it has completed, a
- * wave-specialised abort counted on the device (gsdrAmdWsTakeAborts) fails the call with
+/* Every step entry first checks for a wave-specialised abort counted on the device (a host peek;
+ * when set, the chain's streams are synchronised and the count taken): it fails the call with
  * hipErrorLaunchTimeOut. Cached graphs bake in the kernel policy, the FFT guard ratio and the WS
  * spin limit of their capture; a step after any of them changed recaptures. */
 /* Graphs the chain has instantiated so far (three at creation, plus every StepChunks /
