@@ -408,6 +408,8 @@ def cpu_baseline(wl, seconds_target=8.0):
         "value": (n_out * D) / dt / 1e6,
         "unit": "Msamples/s",
         "cores": threads,
+        # per core, so the all-cores figure of north_star extrapolates (the job gets a CPU share)
+        "per_core_msps": (n_out * D) / dt / 1e6 / threads,
         "host_cpus": os.cpu_count(),
         "affinity_cpus": avail,
         "cpu_model": _cpu_model(),

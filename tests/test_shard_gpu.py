@@ -125,7 +125,10 @@ def test_c5_chain_time_sharded_cascaded_halo(tmp_path, orc, world):
     assert n == L * world * STEPS // (D * Da) and len(want) >= n
     carried, _ = orc.fir_f64(np.abs(au), (FIR_TOL * (rf_bound + am)).astype(np.float32), Da, n)
     bound = carried + FIR_TOL * audio_bound[:n] + 1e-30
-    assert np.all(np.abs(got - want[:n]) <= bound)
+    bad = np.nonzero(np.abs(got - want[:n]) > bound)[0]
+    per = L // (D * Da)  # outputs per rank per step
+    assert len(bad) == 0, (len(bad), [(int(i), int(i // per % world), int(i // per // world), float(got[i]),
+                                       float(want[i]), float(bound[i])) for i in bad[:6]])
 
 
 def test_c5_chain_single_rank_one_launch_matches_split(orc):

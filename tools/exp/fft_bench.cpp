@@ -27,6 +27,20 @@ VARIANT_DECLS
 
 typedef hipError_t (*LaunchFn)(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t);
 
+// two tones like bench.py's synthetic C3 input (gsdrSynthWidebandCf32: exp(j 2 pi f1 n) +
+// 0.5 exp(j 2 pi f2 n) + noise), selected with FFT_BENCH_DATA=twotone
+__global__ void fillTwoTone(float* x, size_t n, uint64_t seed, float noise) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const double s = (double)(i / 2);
+    const double p1 = 2.0 * M_PI * fmod(0.013 * s, 1.0), p2 = 2.0 * M_PI * fmod(0.31 * s, 1.0);
+    uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 31;
+    const double t = (i & 1) ? sin(p1) + 0.5 * sin(p2) : cos(p1) + 0.5 * cos(p2);
+    x[i] = (float)t + noise * ((float)(int32_t)(z >> 32) * (1.0f / 2147483648.0f));
+  }
+}
+
 __global__ void fillKernel(float* x, size_t n, uint64_t seed, float noise) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const double ph = 2.0 * M_PI * fmod(0.013 * (double)(i / 2), 1.0);
@@ -213,7 +227,11 @@ int main() {
       hipMemcpy(x, h.data(), inBytes, hipMemcpyHostToDevice);
     } else {
       // FFT_BENCH_NOISE: amplitude of the uniform noise on the tone (default 0.01; ~1 is wideband)
-      fillKernel<<<1024, 256>>>((float*)x, 2 * nIn, 12345, getenv("FFT_BENCH_NOISE") ? (float)atof(getenv("FFT_BENCH_NOISE")) : 0.01f);
+      const float noise = getenv("FFT_BENCH_NOISE") ? (float)atof(getenv("FFT_BENCH_NOISE")) : 0.01f;
+      if (getenv("FFT_BENCH_DATA") && strcmp(getenv("FFT_BENCH_DATA"), "twotone") == 0)
+        fillTwoTone<<<1024, 256>>>((float*)x, 2 * nIn, 12345, noise);
+      else
+        fillKernel<<<1024, 256>>>((float*)x, 2 * nIn, 12345, noise);
     }
     std::vector<float> ht(sh.T);
     for (size_t j = 0; j < sh.T; ++j) {
