@@ -477,9 +477,29 @@ def spawn_ranks(n, share_gpu=False):
                        start_method="spawn")
 
 
+SETTLE_S = 0.25  # untimed settle before the warm-up steps (see settle)
+
+
+def settle(step, seconds=SETTLE_S):
+    """Run `step` untimed for ~`seconds`: after idle the GPU needs ~10-20 ms of load to leave its
+    low-clock power state - the first ~20-30 C3 launches take 0.66 ms instead of 0.48 ms
+    (profiles/r03/exp/c3_bench_loop_probe.log) - so 5 warm-up steps alone left the timed steps in
+    the ramp. Nothing timed is skipped: the K timed steps still do the full work."""
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds and n < 4096:
+        step()
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+
+
 def timed_steps(chain, steps, warmup, world, backend, device, local, ops):
-    """W untimed steps, then K steps between barrier + synchronize on both sides; the max over ranks
-    of the wall time, and the mean per-step HIP-event time of the timed kernel."""
+    """A short settle, W untimed warm-up steps, then K steps between barrier + synchronize on both
+    sides; the max over ranks of the wall time, and the mean per-step HIP-event time of the timed
+    kernel."""
+    settle(chain.step)
     for _ in range(warmup):
         chain.step()
     torch.cuda.synchronize()
@@ -523,6 +543,7 @@ def mixed_vs_plain(ops, chain, reps=10):
     x, n = chain.slot.buf, chain.geom.outputs
     out = torch.empty(n, dtype=torch.float32, device=x.device)
     ts = {"plain": [], "mixed": []}
+    settle(lambda: ops.fir(chain.taps, x, chain.D, n, out=out, am=True), 0.1)
     for _ in range(2):
         for kind in ("plain", "mixed"):
             mix = (0.3, -2 * np.pi * 0.0731) if kind == "mixed" else None
@@ -555,6 +576,11 @@ def node_path(ops, device, kernel_value, segments=5, warmup=1):
                        "device sink, SteppingDriver.doFilter, one 2^28-sample segment per step",
            "kernel_line_msps": kernel_value}
     steps = segments - warmup
+    # a C3-sized launch to keep the GPU out of its idle clock state before each timed node run
+    probe_n = 1 << 22
+    taps_d = torch.from_numpy(taps).to(device)
+    probe_x = torch.zeros((probe_n - 1) * D + T, dtype=torch.complex64, device=device)
+    probe_out = torch.empty(probe_n, dtype=torch.float32, device=device)
     for fuse in (True, False):
         q = graph.Queue(device.index)
         fir = graph.Node.fir(q, taps, D, graph.SAMPLE_FLOAT_COMPLEX)
@@ -574,6 +600,7 @@ def node_path(ops, device, kernel_value, segments=5, warmup=1):
         for _ in range(warmup):
             drv.do_filter()
         q.sync()
+        settle(lambda: ops.fir(taps_d, probe_x, D, probe_n, out=probe_out, am=True), 0.1)
         # outputs delivered in the timed steps: the Fir's outputs consumed minus what still waits in
         # the AM window (unfused steps need not line up with segments)
         fir0, am0 = fir.output_size()[0] // 8, am.output_size()[0] // 4
