@@ -46,6 +46,8 @@ def _rank_main(rank, world, port, kind, out_dir):
     # stalled far longer than on a GPU of its own: give them room, and fail loudly on any abort
     ops.set_ws_spin_limit(1 << 28)
     ops.ws_aborts(reset=True)
+    if os.environ.get("GSDR_TEST_POLICY"):  # diagnostics: run the ranks under a kernel policy
+        ops.set_kernel_policy(int(os.environ["GSDR_TEST_POLICY"]))
     outs = []
     if kind == "c4":
         T, D, L = 1023, 1, 20_000
@@ -58,10 +60,14 @@ def _rank_main(rank, world, port, kind, out_dir):
         ring = HaloRing(geom, buf[:H], seg[L - H:], incoming, stage=True)
         y = torch.empty(geom.outputs, dtype=torch.complex64, device=dev)
         hb = geom.head_outputs
+        primed = None
         if rank == 0:
             ops.synth_wideband_cf32(0xC4, 0.013, 0.31, 0, H, out=buf[:H])  # primed history
+            primed = buf[:H].cpu().numpy().copy()
+        inputs = []
         for step in range(STEPS):
             ops.synth_wideband_cf32(0xC4, 0.013, 0.31, H + geom.segment_start(step), L, out=seg)
+            inputs.append(seg.cpu().numpy().copy())
             ring.step(lambda: ops.fir(taps, seg[geom.bulk_input_offset():], D, geom.outputs - hb, out=y[hb:]),
                       lambda: ops.fir(taps, buf, D, hb, out=y[:hb]))
             torch.cuda.synchronize()
@@ -73,10 +79,14 @@ def _rank_main(rank, world, port, kind, out_dir):
         au = torch.from_numpy(orc.lowpass_taps(Ta, 0.02)).to(dev)
         sh = AmChainShard(geom, rf, au, dev, stage=True)
         H = geom.halo
+        primed = None
         if rank == 0:
             ops.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, H, out=sh.buf[: 2 * H])  # primed history
+            primed = sh.buf[: 2 * H].cpu().numpy().copy()
+        inputs = []
         for step in range(STEPS):
             ops.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, H + geom.segment_start(step), L, out=sh.seg)
+            inputs.append(sh.seg.cpu().numpy().copy())
             out = sh.step()
             torch.cuda.synchronize()
             outs.append(out.cpu().numpy().copy())
@@ -84,24 +94,34 @@ def _rank_main(rank, world, port, kind, out_dir):
     if aborts:
         raise RuntimeError(f"rank {rank}: {aborts} wave-specialised hand-off aborts")
     np.save(os.path.join(out_dir, f"{kind}_rank{rank}.npy"), np.stack(outs))
+    # the stream as the GPU generated it (the oracle's float64 chain runs on exactly these samples:
+    # the host restatement of the synthetic source may round a rare int8 sample to the neighbouring
+    # code - GPU sincos vs libm in the last ulp - which is not what this test is about)
+    np.save(os.path.join(out_dir, f"{kind}_in_rank{rank}.npy"), np.stack(inputs))
+    if rank == 0:
+        np.save(os.path.join(out_dir, f"{kind}_halo.npy"), primed)
     dist.barrier()
     dist.destroy_process_group()
 
 
 def _run(kind, tmp_path, world):
+    """(outputs in stream order, the input stream the ranks generated: primed halo + segments)."""
     import torch.multiprocessing as mp
     mp.start_processes(_rank_main, args=(world, _free_port(), kind, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     per = [np.load(os.path.join(tmp_path, f"{kind}_rank{r}.npy")) for r in range(world)]
-    return np.concatenate([per[r][s] for s in range(STEPS) for r in range(world)])
+    ins = [np.load(os.path.join(tmp_path, f"{kind}_in_rank{r}.npy")) for r in range(world)]
+    stream = np.concatenate([np.load(os.path.join(tmp_path, f"{kind}_halo.npy"))] +
+                            [ins[r][s] for s in range(STEPS) for r in range(world)])
+    return np.concatenate([per[r][s] for s in range(STEPS) for r in range(world)]), stream
 
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_c4_shape_time_sharded_on_hip(tmp_path, orc, world):
     T, D, L = 1023, 1, 20_000
-    got = _run("c4", tmp_path, world)
+    got, stream = _run("c4", tmp_path, world)
     n = L * world * STEPS
-    stream = orc.synth_wideband_cf32(0xC4, 0.013, 0.31, 0, T - 1 + n)
+    assert len(stream) == T - 1 + n
     y64, bound = orc.fir_f64(orc.lowpass_taps(T, 0.04, "blackman"), stream, D, n // D)
     assert len(got) == len(y64)
     err = np.abs(got.astype(np.complex128) - y64)
@@ -114,8 +134,8 @@ def test_c5_chain_time_sharded_cascaded_halo(tmp_path, orc, world):
     T, D, Ta, Da, L = 1023, 10, 255, 20, 40_000
     H = ChainShardGeometry(0, world, L, T, D, Ta, Da).halo
     assert H == 3600  # (Ta - 1) D + T - 1 = 3562, rounded up to a multiple of D Da
-    got = _run("c5", tmp_path, world)
-    padded = orc.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, H + L * world * STEPS)  # primed stream
+    got, padded = _run("c5", tmp_path, world)  # the primed stream the ranks generated
+    assert len(padded) == 2 * (H + L * world * STEPS)
     rf, au = orc.lowpass_taps(T, 0.04, "blackman"), orc.lowpass_taps(Ta, 0.02)
     x = orc.int8_to_float(padded).view(np.complex64)
     y, rf_bound = orc.fir_f64(rf, x, D)
