@@ -488,7 +488,7 @@ Status HipMemcpyFilter::readOutput(IBuffer** portOutputBuffers, size_t portCount
   return consumeInputBytesAndMoveUsedToStart(0, n);
 }
 
-// ---- host egress (AacFileWriter.cpp:267-280 minus the codec; Waiter.cpp:34-50) ---------------------------
+// ---- device sink: the end of a chain whose output stays in HBM --------------------------------------
 Result<Sink> DeviceSink::create(size_t preferredBytes, ICudaCommandQueue* queue, IFactories* factories) noexcept {
   NON_NULL_PARAM_OR_RET(queue);
   Ref<IRelocatableResizableBufferFactory> windows;
@@ -501,6 +501,21 @@ Result<Sink> DeviceSink::create(size_t preferredBytes, ICudaCommandQueue* queue,
 DeviceSink::DeviceSink(size_t preferredBytes, IRelocatableResizableBufferFactory* windows, IBufferSliceFactory* slices,
                        ICudaCommandQueue* queue) noexcept
     : BaseSink(windows, slices, 1), mQueue(queue), mPreferred(preferredBytes) {}
+
+Result<IBuffer> DeviceSink::requestBuffer(size_t port, size_t numBytes) noexcept {
+  if (!inputPortsInitialized()) {  // creates the port windows on first use
+    Ref<IBuffer> lazy;
+    UNWRAP_OR_FWD_RESULT(lazy, getPortInputBuffer(port));
+  }
+  if (port < inputWindowCount() && !inputWindowCheckedOut(port)) {
+    IRelocatableResizableBuffer* b = inputWindow(port);
+    if (b != nullptr && b->range()->remaining() < numBytes) {
+      if (b->range()->offset() != 0) FWD_IN_RESULT_IF_ERR(b->relocateUsedToStart());
+      if (b->range()->remaining() < numBytes) FWD_IN_RESULT_IF_ERR(b->resize(b->range()->endOffset() + numBytes));
+    }
+  }
+  return BaseSink::requestBuffer(port, numBytes);
+}
 
 Status DeviceSink::commitBuffer(size_t port, size_t byteCount) noexcept {
   FWD_IF_ERR(BaseSink::commitBuffer(port, byteCount));

@@ -239,6 +239,10 @@ class DeviceSink final : public BaseSink, public IGraphStepState {
   bool saveStepState(GraphNodeState& out) const noexcept final { return saveSinkWindows(*this, out); }
   Status restoreStepState(const GraphNodeState& in) noexcept final { return restoreSinkWindows(*this, in); }
   static Result<Sink> create(size_t preferredBytes, ICudaCommandQueue* queue, IFactories* factories) noexcept;
+  // grows the window to exactly the request, as the reference's BaseSink does (BaseSink.cpp:75-77):
+  // the window never holds history (every commit is consumed), so the 2x headroom BaseSink takes
+  // for appending steps buys nothing here and would let a step run past the preferred size
+  Result<IBuffer> requestBuffer(size_t port, size_t numBytes) noexcept final;
   Status commitBuffer(size_t port, size_t byteCount) noexcept final;
   size_t preferredInputBufferSize(size_t port) noexcept final { return mPreferred; }
 
