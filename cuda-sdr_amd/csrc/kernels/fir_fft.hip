@@ -136,6 +136,12 @@ __device__ __forceinline__ f2 cmul2(f2 a, f2 b, f2 t) {
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
   return r;
 }
+// second half of a * conj(b) (the first half is cmul1)
+__device__ __forceinline__ f2 cmulc2(f2 a, f2 b, f2 t) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
 __device__ __forceinline__ f2 cmac(f2 a, f2 b, f2 acc) {  // acc + a * b
   f2 t, r;
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(a), "v"(b), "v"(acc));
@@ -730,17 +736,22 @@ __device__ __forceinline__ void drainBlockLoads(const PrefetchCf<D>& P, Rows<D, 
     }
 }
 
-// ---- D = 1: eight output phases per block from eight shared input-phase spectra -----------------
+// ---- D = 1: a 4096-point overlap-save FFT as eight 512-point FFTs and a radix-8 phase stage ------
 // With k = 8m + r and j = 8q + p (p, r < 8), y[8m + r] = sum_p sum_q h_p[q] x_{(p+r) mod 8}[m + q + c],
 // c = (p + r >= 8), x_t[n] = x[8n + t], h_p[q] = h[8q + p]: each output phase r is an 8-phase
 // polyphase correlation of the SAME input phases, some advanced by one row. A block of 512 rows (8
-// samples each) is transformed once per input phase (8 forward FFTs, spectra kept in registers in
-// place of the rows); output phase r is Y_r = sum_{p < 8-r} X_{p+r} G_p + w^k sum_{p >= 8-r}
-// X_{p+r-8} G_p (w^k = exp(+2 pi i k / 512): the one-row advance) and one inverse FFT, valid for
-// m < V = 512 - Q. Per block 8 V outputs for 16 FFTs - against D x (one FFT per phase) + 1 per V
-// outputs at D >= 2 - so the long D = 1 filter (C4: 1023 taps) runs at a few hundred flops per
-// sample instead of 4 T.
-constexpr int kOmega = 512;  // w^k table, per-lane float4 pairs like G
+// samples each) is transformed once per input phase (8 forward 512-point FFTs X_t, in registers in
+// place of the rows). Per frequency k, Y_r = sum_t X_t G_{(t - r) mod 8} (w^k if t < r), w^k =
+// exp(+2 pi i k / 512) the one-row advance. With alpha = exp(+2 pi i k / 4096) (alpha^8 = w^k) the
+// twist X~_t = alpha^-t X_t, G~_s = alpha^s G_s turns that into a plain circular correlation over
+// the phase index, alpha^-r Y_r = sum_s X~_{(r + s) mod 8} G~_s, which an 8-point DFT over the
+// phases diagonalises: A_f = DFT8_t(X~_t), B_f = (1/8) sum_s G~_s W8^-fs (built once per launch, in
+// place of G), alpha^-r Y_r = IDFT8_f(A_f B_f). Per frequency 7 + 8 + 7 complex products and two
+// in-register 8-point DFTs instead of 64 complex MACs and 7 twists (r02-r03a), and 88 instead of 256
+// table reads per lane and block. (This is the decimation-in-time radix-8 stage of a 4096-point
+// FFT of the block and its decimation-in-frequency inverse: the same overlap-save, valid for
+// m < V = 512 - Q.) Then one inverse 512-point FFT per output phase.
+constexpr int kTwD1 = 7 * 8 * 64;  // alpha^-t, t = 1..7: per-lane float4 pairs like G
 
 template <int EPI>
 __device__ void directBlockD1(const Args& a, int64_t b, int l) {
@@ -767,23 +778,60 @@ __device__ void directBlockD1(const Args& a, int64_t b, int l) {
   }
 }
 
-// The w^k table (layout F, per-lane float4 pairs like G), filled by the workgroup's threads.
-__device__ __forceinline__ void fillOmega(f2* omegaAll, int threads) {
-  for (int n = threadIdx.x; n < kOmega; n += threads) {
-    // complex n = ((d / 2) 64 + lane) 2 + (d & 1); layout F: lane = 8 k0 + c holds k0 + 8 c + 64 d
+// After buildTables (G_s in layout F at gAll, barrier passed): G_s -> B_f in place and the twist
+// table alpha^-t, in double, rounded once. Complex slot n of a phase's 512 (layout F: n = ((d / 2)
+// 64 + lane) 2 + (d & 1), frequency k = k0 + 8 c + 64 d for lane 8 k0 + c) is read and written only
+// by thread n mod threads, so no barrier is needed between the reads and the writes.
+__device__ __forceinline__ void buildPhaseTablesD1(f2* gAll, f2* twist, int threads) {
+  for (int n = threadIdx.x; n < kM; n += threads) {
     const int lane = (n >> 1) & 63, d = 2 * (n >> 7) + (n & 1);
     const int k = (lane >> 3) + 8 * (lane & 7) + 64 * d;
-    double sn, cs;
-    sincospi(2.0 * k / kM, &sn, &cs);
-    omegaAll[n] = f2{(float)cs, (float)sn};
+    double gr[8], gi[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {  // G~_s = alpha^s G_s
+      double sn, cs;
+      sincospi(2.0 * (double)(k * s) / 4096.0, &sn, &cs);
+      const f2 g = gAll[s * kM + n];
+      gr[s] = (double)g.x * cs - (double)g.y * sn;
+      gi[s] = (double)g.x * sn + (double)g.y * cs;
+    }
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {  // B_f = (1/8) sum_s G~_s exp(+2 pi i f s / 8)
+      double br = 0.0, bi = 0.0;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        double sn, cs;
+        sincospi((double)((f * s) & 7) / 4.0, &sn, &cs);
+        br += gr[s] * cs - gi[s] * sn;
+        bi += gr[s] * sn + gi[s] * cs;
+      }
+      gAll[f * kM + n] = f2{(float)(br * 0.125), (float)(bi * 0.125)};
+    }
+#pragma unroll
+    for (int t = 1; t < 8; ++t) {
+      double sn, cs;
+      sincospi(-2.0 * (double)(k * t) / 4096.0, &sn, &cs);
+      twist[(t - 1) * kM + n] = f2{(float)cs, (float)sn};
+    }
   }
 }
 
-// One D = 1 block: the eight input-phase spectra, then per output phase the spectral sum, one
+// Eight factors of one table row (t, or f for B) for this lane: f4 pairs at (row 4 + d / 2) 64 from
+// tab, which already points at this lane's column.
+__device__ __forceinline__ void loadRow8(f2 (&v)[8], const f4* tab, int row) {
+#pragma unroll
+  for (int d = 0; d < 8; d += 2) {
+    const f4 u = tab[(row * 4 + d / 2) * 64];
+    v[d] = f2{u.x, u.y};
+    v[d + 1] = f2{u.z, u.w};
+  }
+}
+
+// One D = 1 block: the eight input-phase spectra, the phase stage, then per output phase one
 // inverse FFT and the stores.
 template <int EPI>
 __device__ __forceinline__ void convolveBlockD1(const Args& a, const Rows<8, kCf32>& R, int64_t b, const Lds& L,
-                                                const f4* omega, int l) {
+                                                const f4* twist, int l) {
   constexpr int D = 8;
   // the eight input-phase spectra, in place of the rows
   f2 X[D][8];
@@ -800,48 +848,60 @@ __device__ __forceinline__ void convolveBlockD1(const Args& a, const Rows<8, kCf
 #pragma unroll
       for (int d = 0; d < 8; ++d) X[p + n][d] = z[n][d];
   }
+  // X~_t = alpha^-t X_t (the halves of each row's eight products issued stage-interleaved: a
+  // v_pk_fma right behind the one that writes its operand costs an s_nop, and one wave per SIMD
+  // has nothing to hide it behind)
+#pragma unroll
+  for (int t = 1; t < D; ++t) {
+    f2 w[8], u[8];
+    loadRow8(w, twist, t - 1);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) u[d] = cmul1(X[t][d], w[d]);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) X[t][d] = cmul2(X[t][d], w[d], u[d]);
+  }
+  // A_f = DFT8 over the phases, times B_f, inverse DFT8: alpha^-r Y_r in X[r]
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    f2 z[8];
+#pragma unroll
+    for (int t = 0; t < D; ++t) z[t] = X[t][d];
+    dft8<false>(z);
+#pragma unroll
+    for (int f = 0; f < D; ++f) X[f][d] = z[f];
+  }
+#pragma unroll
+  for (int f = 0; f < D; ++f) {
+    f2 g[8], u[8];
+    loadRow8(g, L.g + l, f);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) u[d] = cmul1(X[f][d], g[d]);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) X[f][d] = cmul2(X[f][d], g[d], u[d]);
+  }
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    f2 z[8];
+#pragma unroll
+    for (int f = 0; f < D; ++f) z[f] = X[f][d];
+    dft8<true>(z);
+#pragma unroll
+    for (int r = 0; r < D; ++r) X[r][d] = z[r];
+  }
   const int64_t row0 = b * (int64_t)a.V;
 #pragma unroll
   for (int r = 0; r < D; ++r) {
-    f2 acc[1][8], sh[8];
+    f2 acc[1][8];
+    if (r > 0) {  // Y_r = alpha^r (alpha^-r Y_r): times the conjugate of the twist row r
+      f2 w[8], u[8];
+      loadRow8(w, twist, r - 1);
 #pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      acc[0][d] = f2{0.0f, 0.0f};
-      sh[d] = f2{0.0f, 0.0f};
-    }
+      for (int d = 0; d < 8; ++d) u[d] = cmul1(X[r][d], w[d]);
 #pragma unroll
-    for (int p = 0; p < D; ++p) {
-      f2 g[8];
+      for (int d = 0; d < 8; ++d) acc[0][d] = cmulc2(X[r][d], w[d], u[d]);
+    } else {
 #pragma unroll
-      for (int d = 0; d < 8; d += 2) {
-        const f4 v = L.g[(p * 4 + d / 2) * 64 + l];
-        g[d] = f2{v.x, v.y};
-        g[d + 1] = f2{v.z, v.w};
-      }
-      const int t = p + r;
-      // the two halves of the eight complex MACs issued stage-interleaved: a v_pk_fma right
-      // behind the one that writes its operand costs an s_nop (one wave per SIMD: nothing hides it)
-      f2 u[8];
-#pragma unroll
-      for (int d = 0; d < 8; ++d) u[d] = t < D ? cmac1(X[t][d], g[d], acc[0][d]) : cmac1(X[t - D][d], g[d], sh[d]);
-#pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        if (t < D) acc[0][d] = cmul2(X[t][d], g[d], u[d]);
-        else sh[d] = cmul2(X[t - D][d], g[d], u[d]);
-      }
-    }
-    if (r > 0) {  // the one-row advance of the wrapped phases
-      f2 om[8], u[8];
-#pragma unroll
-      for (int d = 0; d < 8; d += 2) {
-        const f4 v = omega[(d / 2) * 64];
-        om[d] = f2{v.x, v.y};
-        om[d + 1] = f2{v.z, v.w};
-      }
-#pragma unroll
-      for (int d = 0; d < 8; ++d) u[d] = cmac1(sh[d], om[d], acc[0][d]);
-#pragma unroll
-      for (int d = 0; d < 8; ++d) acc[0][d] = cmul2(sh[d], om[d], u[d]);
+      for (int d = 0; d < 8; ++d) acc[0][d] = X[0][d];
     }
     ifft512(acc, L, l);
     // outputs 8 (row0 + m) + r for m < nv (wave-uniform bound and base, 32-bit lane math)
@@ -870,14 +930,15 @@ firFftD1PfKernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) f2 lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   f2* twAll = lds + D * 8 * 64;
-  f2* omegaAll = twAll + kTw + kPfWaves * scratchComplex<D>(kCf32);
+  f2* twistAll = twAll + kTw + kPfWaves * scratchComplex<D>(kCf32);
   Lds L;
   L.g = reinterpret_cast<f4*>(lds);
   L.tw = reinterpret_cast<const f4*>(twAll) + l;
   L.scratch = twAll + kTw + w * scratchComplex<D>(kCf32);
-  fillOmega(omegaAll, kPfWaves * kWave);
-  buildTables<D, kCf32, kPfWaves>(a, twAll, L, w, l);  // (its barriers also publish the w^k table)
-  const f4* omega = reinterpret_cast<const f4*>(omegaAll) + l;
+  buildTables<D, kCf32, kPfWaves>(a, twAll, L, w, l);
+  buildPhaseTablesD1(lds, twistAll, kPfWaves * kWave);
+  __syncthreads();
+  const f4* twist = reinterpret_cast<const f4*>(twistAll) + l;
   const int64_t stride = (int64_t)gridDim.x * kPfWaves;
   int64_t b = (int64_t)blockIdx.x * kPfWaves + w;
   PrefetchCf<D> P;
@@ -892,7 +953,7 @@ firFftD1PfKernel(Args a) {
       directBlockD1<EPI>(a, b, l);
       continue;
     }
-    convolveBlockD1<EPI>(a, R, b, L, omega, l);
+    convolveBlockD1<EPI>(a, R, b, L, twist, l);
   }
 }
 
@@ -929,7 +990,7 @@ template <int EPI>
 hipError_t launchD1(fftfir::Args a, hipStream_t stream) {
   using namespace fftfir;
   auto kernel = firFftD1PfKernel<EPI>;
-  const size_t lds = (size_t)(8 * 8 * 64 + kTw + kPfWaves * scratchComplex<8>(kCf32) + kOmega) * sizeof(f2);
+  const size_t lds = (size_t)(8 * 8 * 64 + kTw + kPfWaves * scratchComplex<8>(kCf32) + kTwD1) * sizeof(f2);
   // set per launch (cheap): a once-per-process flag would race between threads and miss other devices
   const hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
