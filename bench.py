@@ -560,13 +560,15 @@ def mixed_vs_plain(ops, chain, reps=10):
             "plain_ms": plain, "mixed_ms": mixed, "mixed_over_plain": mixed / plain}
 
 
-def node_path(ops, device, kernel_value, segments=5, warmup=1):
+def node_path(ops, device, kernel_value, segments=11, warmup=1):
     """C3 through the reference's filter-graph API (getFactoriesSingleton nodes, SteppingDriver):
     Fir(real taps, FloatComplex, D = 10) -> QuadAmDemod -> a device sink taking one C3 segment of AM
     output per step. The Fir window is pre-filled with `segments` C3 segments (2^28 - 6 samples each,
-    outside the timed region: an upstream node would write them there); each driver step then moves
-    one segment: with fusion ONE gsdrFirFCAmDemod launch, without it the reference's Fir and
-    QuadAmDemod launches with the cf32 intermediate in the AM window. Also the host time of one
+    outside the timed region: an upstream node would write them there); each fused driver step then
+    moves one segment (the device sink grows its window exactly to the request) in ONE
+    gsdrFirFCAmDemod launch; unfused, the reference's Fir and QuadAmDemod launches with the cf32
+    intermediate in the AM window, which the Fir may fill ahead by its headroom (outputs are counted
+    from the windows, not assumed). Also the host time of one
     driver step, eager vs replayed (doFilterGraphed), on 1 MiB pushes (the reference's chunk)."""
     from gpusdr import graph
     desc, kind, L, T, D, cutoff, window, fs = WORKLOADS["c3"]
@@ -576,8 +578,10 @@ def node_path(ops, device, kernel_value, segments=5, warmup=1):
                        "device sink, SteppingDriver.doFilter, one 2^28-sample segment per step",
            "kernel_line_msps": kernel_value}
     steps = segments - warmup
-    # a C3-sized launch to keep the GPU out of its idle clock state before each timed node run
-    probe_n = 1 << 22
+    # full C3-sized launches before each timed node run, as the kernel line settles: the clock under
+    # the board's power cap only reaches its steady state after ~10-20 ms of full load, and a
+    # lighter settle would time the first steps at a burst clock the kernel line never sees
+    probe_n = n_out
     taps_d = torch.from_numpy(taps).to(device)
     probe_x = torch.zeros((probe_n - 1) * D + T, dtype=torch.complex64, device=device)
     probe_out = torch.empty(probe_n, dtype=torch.float32, device=device)
@@ -600,7 +604,7 @@ def node_path(ops, device, kernel_value, segments=5, warmup=1):
         for _ in range(warmup):
             drv.do_filter()
         q.sync()
-        settle(lambda: ops.fir(taps_d, probe_x, D, probe_n, out=probe_out, am=True), 0.1)
+        settle(lambda: ops.fir(taps_d, probe_x, D, probe_n, out=probe_out, am=True), SETTLE_S)
         # outputs delivered in the timed steps: the Fir's outputs consumed minus what still waits in
         # the AM window (unfused steps need not line up with segments)
         fir0, am0 = fir.output_size()[0] // 8, am.output_size()[0] // 4

@@ -75,6 +75,7 @@ struct Args {
   float guardRatio;     // direct-form fallback when max/min row-group level exceeds this
   uint64_t mixPhase0;   // fused frequency shifter (kernels with MIX): sample n of `in` is multiplied
   uint64_t mixStep;     // by exp(j theta(n)), theta(n) = 2 pi (mixPhase0 + n mixStep) / 2^64
+  int32_t outAligned;   // `out` is 16-byte aligned (the D = 1 kernel's row-unit stores)
 };
 
 // ---- fused frequency shifter -----------------------------------------------------------------------
@@ -318,10 +319,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t blockRsrc(const void* base, in
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
 }
 
+// cf32 row-group image: row r of the group at 16-byte unit r kRowUnits<D> (D / 2 units of data).
+// Rows D * 8 bytes apart put the ds_read_b128 of lanes 64 / (D / 2) apart on the same banks when D / 2
+// is a power of two (D = 8, the D = 1 kernel: 4-way, 15 % of its LDS cycles in SQ_LDS_BANK_CONFLICT);
+// one pad unit per row then spreads a 16-lane group over 16 distinct bank quads.
+#ifndef GSDR_FFT_PADROWS
+#define GSDR_FFT_PADROWS 1
+#endif
+template <int D>
+constexpr int kRowUnits = D / 2 + ((GSDR_FFT_PADROWS && (D == 4 || D == 8)) ? 1 : 0);
+
 template <int D>
 constexpr int scratchComplex(int input) {
-  // two exchange areas (2 x kXch) | cf32 row-group image (64 D) | int8 block image (512 D x 2 B + 16)
-  return input == kCf32 ? (64 * D > 2 * kXch ? 64 * D : 2 * kXch)
+  // two exchange areas (2 x kXch) | cf32 row-group image (64 rows x kRowUnits 16-byte units) | int8
+  // block image (512 D x 2 B + 16)
+  return input == kCf32 ? (128 * kRowUnits<D> > 2 * kXch ? 128 * kRowUnits<D> : 2 * kXch)
                         : ((1024 * D + 16) / 8 > 2 * kXch ? (1024 * D + 16 + 7) / 8 : 2 * kXch);
 }
 
@@ -429,12 +441,16 @@ __device__ __forceinline__ void transposeRows(Rows<D, kCf32>& R, f2* s, int l) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     f4* s4 = reinterpret_cast<f4*>(s);
+    constexpr int H = D / 2, RU = kRowUnits<D>;
 #pragma unroll
-    for (int i = 0; i < D / 2; ++i) s4[i * 64 + l] = f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
+    for (int i = 0; i < H; ++i) {  // unit u = 64 i + l of the group: row u / H, unit u % H of it
+      const int u = i * 64 + l;
+      s4[RU == H ? u : (u / H) * RU + u % H] = f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
+    }
     ldsOrder();
 #pragma unroll
-    for (int p = 0; p < D; p += 2) {  // row l: 16-byte reads (D even), lanes 16 D bytes apart
-      const f4 u = reinterpret_cast<const f4*>(s)[(l * D + p) / 2];
+    for (int p = 0; p < D; p += 2) {  // row l: 16-byte reads (D even), lanes 16 RU bytes apart
+      const f4 u = reinterpret_cast<const f4*>(s)[l * RU + p / 2];
       R.v[j][p] = f2{u.x, u.y};
       R.v[j][p + 1] = f2{u.z, u.w};
     }
@@ -753,6 +769,17 @@ __device__ __forceinline__ void drainBlockLoads(const PrefetchCf<D>& P, Rows<D, 
 // m < V = 512 - Q.) Then one inverse 512-point FFT per output phase.
 constexpr int kTwD1 = 7 * 8 * 64;  // alpha^-t, t = 1..7: per-lane float4 pairs like G
 
+// Workgroup i runs on XCD i mod 8 (round-robin dispatch). Logical group (i mod 8) n / 8 + i / 8 puts
+// consecutive logical groups - whose blocks share their overlap rows - on one XCD, so the re-read
+// rows meet in that XCD's L2 rather than travelling from the fabric twice.
+#ifndef GSDR_FFT_XCD
+#define GSDR_FFT_XCD 1
+#endif
+__device__ __forceinline__ int xcdGroup(int i, int n) {
+  if (!GSDR_FFT_XCD || (n & 7) != 0) return i;
+  return (i & 7) * (n >> 3) + (i >> 3);
+}
+
 template <int EPI>
 __device__ void directBlockD1(const Args& a, int64_t b, int l) {
   const int64_t k0 = b * (int64_t)a.V * 8;  // first output of the block
@@ -889,6 +916,8 @@ __device__ __forceinline__ void convolveBlockD1(const Args& a, const Rows<8, kCf
     for (int r = 0; r < D; ++r) X[r][d] = z[r];
   }
   const int64_t row0 = b * (int64_t)a.V;
+  // outputs 8 (row0 + m) + r: row m = l + 64 h of output phase r lands in lane l, register h
+  float am[D][8];  // EPI == kAm: the envelopes (the complex results go back into X[r])
 #pragma unroll
   for (int r = 0; r < D; ++r) {
     f2 acc[1][8];
@@ -904,19 +933,43 @@ __device__ __forceinline__ void convolveBlockD1(const Args& a, const Rows<8, kCf
       for (int d = 0; d < 8; ++d) acc[0][d] = X[0][d];
     }
     ifft512(acc, L, l);
-    // outputs 8 (row0 + m) + r for m < nv (wave-uniform bound and base, 32-bit lane math)
-    const int64_t left = a.nOut - 8 * row0 - r;
-    const int64_t rows = left <= 0 ? 0 : (left + 7) / 8;
-    const int nv = __builtin_amdgcn_readfirstlane((int)(rows < a.V ? rows : a.V));
-    const int64_t base = 8 * row0 + r;
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
-      const int m = l + 64 * h;
-      if (m < nv) {
-        if (EPI == kAm)
-          (reinterpret_cast<float*>(a.out) + base)[8 * m] = amEnvelope(acc[0][h]);
-        else
-          (reinterpret_cast<f2*>(a.out) + base)[8 * m] = acc[0][h];
+      if (EPI == kAm) am[r][h] = amEnvelope(acc[0][h]);
+      else X[r][h] = acc[0][h];
+    }
+  }
+  // row m's eight phases are 8 consecutive outputs: stored as 16-byte units (lanes 32 / 64 bytes
+  // apart, the whole row range of a register h in one sweep) - phase-strided 4-byte stores left
+  // lines partially written and cost 1.31x the output bytes in WRITE_SIZE (C4, r03 profile)
+  const int64_t left = a.nOut - 8 * row0;
+  const int64_t rows = left <= 0 ? 0 : (left + 7) / 8;
+  const int nv = __builtin_amdgcn_readfirstlane((int)(rows < a.V ? rows : a.V));
+  const bool whole = left >= 8 * (int64_t)a.V;  // wave-uniform: every row of the block is complete
+#pragma unroll
+  for (int h = 0; h < 8; ++h) {
+    const int m = l + 64 * h;
+    if (m >= nv) continue;
+    const int64_t k0 = 8 * (row0 + m);
+    if (EPI == kAm) {
+      float* o = reinterpret_cast<float*>(a.out) + k0;
+      if (whole && a.outAligned) {
+        reinterpret_cast<f4*>(o)[0] = f4{am[0][h], am[1][h], am[2][h], am[3][h]};
+        reinterpret_cast<f4*>(o)[1] = f4{am[4][h], am[5][h], am[6][h], am[7][h]};
+      } else {
+#pragma unroll
+        for (int r = 0; r < D; ++r)
+          if (k0 + r < a.nOut) o[r] = am[r][h];
+      }
+    } else {
+      f2* o = reinterpret_cast<f2*>(a.out) + k0;
+      if (whole && a.outAligned) {
+#pragma unroll
+        for (int r = 0; r < D; r += 2) reinterpret_cast<f4*>(o)[r / 2] = f4{X[r][h].x, X[r][h].y, X[r + 1][h].x, X[r + 1][h].y};
+      } else {
+#pragma unroll
+        for (int r = 0; r < D; ++r)
+          if (k0 + r < a.nOut) o[r] = X[r][h];
       }
     }
   }
@@ -940,7 +993,7 @@ firFftD1PfKernel(Args a) {
   __syncthreads();
   const f4* twist = reinterpret_cast<const f4*>(twistAll) + l;
   const int64_t stride = (int64_t)gridDim.x * kPfWaves;
-  int64_t b = (int64_t)blockIdx.x * kPfWaves + w;
+  int64_t b = (int64_t)xcdGroup((int)blockIdx.x, (int)gridDim.x) * kPfWaves + w;
   PrefetchCf<D> P;
   issueBlockLoads<D>(a, b, P, l);
   for (; b < a.nBlocks; b += stride) {
@@ -1056,6 +1109,7 @@ hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t t
     a.inRows = (int64_t)((nOut - 1 + tapCount) / 8);
     a.inScale = 1.0f;
     a.guardRatio = gFftGuard.load(std::memory_order_relaxed);
+    a.outAligned = ((uintptr_t)out & 15) == 0;
     return epi == kEpiAm ? launchD1<kAm>(a, stream) : launchD1<kComplex>(a, stream);
   }
   Args a{};
