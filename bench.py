@@ -230,11 +230,20 @@ class AmChainSharded:
         self.rf_taps = rf
         step_bytes = 2 * (g.halo + L) + 4 * g.rf_outputs + 4 * g.outputs
         self.n_slots = max(1, -(-int(1.5 * MALL_BYTES) // step_bytes))
-        self.slots = [AmChainShard(g, rf, au, device, stage) for _ in range(self.n_slots)]
+        self.single = world == 1
+        if self.single:
+            # one rank: the slots are consecutive views of one input ring, so slot k + 1's halo IS slot
+            # k's segment tail (a live receiver's ring holds its history in front of the new samples);
+            # only the wrap back to slot 0 copies the history. 8 slots: one 7 KB copy per 8 steps.
+            self.n_slots = max(self.n_slots, 8)
+            ring = torch.zeros(2 * (g.halo + self.n_slots * L), dtype=torch.int8, device=device)
+            self.slots = [AmChainShard(g, rf, au, device, stage, buf=ring[2 * k * L: 2 * (k * L + g.halo + L)])
+                          for k in range(self.n_slots)]
+        else:
+            self.slots = [AmChainShard(g, rf, au, device, stage) for _ in range(self.n_slots)]
         for k, sh in enumerate(self.slots):
             ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, g.segment_start(k), L, out=sh.seg)
         self.cur = 0
-        self.single = world == 1
         self.kernel_class = ops.fir_kernel_class(self.slots[0].seg, rf, D, int8_iq=True)
 
     def step(self, ev=None):
@@ -242,8 +251,12 @@ class AmChainSharded:
         nxt = self.slots[(self.cur + 1) % self.n_slots]
         if ev is not None:
             ev[0].record()
-        # one rank: the history goes straight into the next slot's halo
-        sh.step(carry_to=nxt.ring.halo if g.world == 1 else None)
+        # one rank: the next slot's halo already holds this segment's tail, except at the wrap
+        if g.world == 1:
+            last = self.cur == self.n_slots - 1
+            sh.step(carry_to=nxt.ring.halo, carry=last)
+        else:
+            sh.step()
         if ev is not None:
             ev[1].record()
         if self.n_slots > 1 and g.world > 1 and g.rank == 0:
@@ -265,10 +278,11 @@ def kernel_compute(cls, n_out, T, D):
     if cls == "fft":
         fft = 5 * 512 * 9  # nominal 5 N log2 N per 512-point FFT
         kind = "fp32 FFT fast convolution (polyphase overlap-save, 512-point FFTs; nominal 5 N log2 N)"
-        if D == 1:  # firFftD1PfKernel: 8 input-phase FFTs, 8 x 8 spectral MACs, 8 inverse FFTs per block
+        if D == 1:  # firFftD1PfKernel: 8 input-phase FFTs, the phase stage (per frequency 22 complex
+            # products and two 8-point DFTs, nominal 5 N log2 N), 8 inverse FFTs per block
             V = 512 - -(-T // 8)
             blocks = -(-n_out // (8 * V))
-            return kind, blocks * (8 * fft + 64 * 512 * 8 + 8 * fft), FP32_PEAK_TFLOPS
+            return kind, blocks * (8 * fft + 512 * (22 * 6 + 2 * 5 * 8 * 3) + 8 * fft), FP32_PEAK_TFLOPS
         Q = -(-T // D)
         V = 512 - Q + 1
         blocks = -(-n_out // V)

@@ -260,6 +260,28 @@ class HostSinkFactory final : public INodeFactory {
   REF_COUNTED(HostSinkFactory);
 };
 
+// ---- device sink (MI355X extension: the end of a chain whose output stays in HBM) ------------------------
+class DeviceSinkFactory final : public INodeFactory {
+ public:
+  explicit DeviceSinkFactory(IFactories* f) noexcept : mF(f) {}
+  Result<Node> create(const char* jsonParameters) noexcept final {
+    try {
+      Json p;
+      if (!parseParams(jsonParameters, p)) return ERR_RESULT(Status_ParseError);
+      Ref<ICudaCommandQueue> q;
+      UNWRAP_OR_FWD_RESULT(q, queueFromParams(mF, p));
+      const Json* pb = p.get("preferredBytes");  // optional; 0 / absent: the device-node default
+      const size_t preferred = pb != nullptr && pb->isNumber() && pb->number() > 0 ? (size_t)pb->number() : 0;
+      return ResultCast<Node>(DeviceSink::create(preferred, q.get().get(), mF));
+    }
+    IF_CATCH_RETURN_RESULT;
+  }
+
+ private:
+  IFactories* const mF;
+  REF_COUNTED(DeviceSinkFactory);
+};
+
 // ---- out-of-scope factories: valid objects whose creators report Status_NotFound ----------------------------
 #define GS_OUT_OF_SCOPE(what__)            \
   do {                                     \
@@ -581,6 +603,11 @@ GS_EXPORT Status registerDefaultNodeFactories() noexcept {
     Ref<INodeFactory> hostSink(new (std::nothrow) HostSinkFactory(F));
     if (hostSink == nullptr) return Status_OutOfMemory;
     FWD_IF_ERR(registerNodeFactory("HostSink", hostSink.get().get()));
+  }
+  {
+    Ref<INodeFactory> deviceSink(new (std::nothrow) DeviceSinkFactory(F));
+    if (deviceSink == nullptr) return Status_OutOfMemory;
+    FWD_IF_ERR(registerNodeFactory("DeviceSink", deviceSink.get().get()));
   }
   // extension: the RF -> PCM component by name (the reference only reaches it through IFactories)
   FWD_IF_ERR(registerNodeFactory("RfToPcmAudio", F->getRfToPcmAudioFactory()));

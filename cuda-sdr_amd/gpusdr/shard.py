@@ -210,11 +210,18 @@ class AmChainShard:
     reaching into the halo), then the audio FIR (gsdrFirFF) over the step's AM samples.
     Weak scaling: every rank processes seg_len samples per step."""
 
-    def __init__(self, geom: ChainShardGeometry, rf_taps, audio_taps, device, stage: bool = False):
+    def __init__(self, geom: ChainShardGeometry, rf_taps, audio_taps, device, stage: bool = False, buf=None):
+        """`buf`: an int8 view of 2 (halo + seg_len) bytes to work in (default: a fresh buffer). Views
+        of one ring laid out segment after segment let a single rank read its history in place: the
+        next view's halo IS this view's segment tail (step(carry=False))."""
         import torch
         self.geom, self.rf_taps, self.audio_taps = geom, rf_taps, audio_taps
         H, L = geom.halo, geom.seg_len
-        self.buf = torch.zeros(2 * (H + L), dtype=torch.int8, device=device)
+        if buf is None:
+            buf = torch.zeros(2 * (H + L), dtype=torch.int8, device=device)
+        if buf.dtype != torch.int8 or buf.numel() != 2 * (H + L):
+            raise ValueError(f"AmChainShard: buf must be int8 with {2 * (H + L)} elements")
+        self.buf = buf
         self.seg = self.buf[2 * H:]
         incoming = (torch.zeros(2 * H, dtype=torch.int8, device=device)
                     if geom.world > 1 and geom.rank == 0 else None)
@@ -233,16 +240,18 @@ class AmChainShard:
         g = self.geom
         ops.fir(self.rf_taps, self.buf, g.decimation, g.head_rf, out=self.am[: g.head_rf], am=True, int8_iq=True)
 
-    def step(self, carry_to=None):
+    def step(self, carry_to=None, carry: bool = True):
         """One step over the segment currently in self.seg; the audio lands in self.out. A single
         rank (the halo is its own history) runs the RF stage as ONE launch over [halo | segment]
         (the halo is a multiple of D: the same outputs as the bulk and head launches) and copies the
-        segment's tail to `carry_to` (default: its own halo), the next step's history."""
+        segment's tail to `carry_to` (default: its own halo), the next step's history - unless
+        `carry` is False because the next step's halo already aliases the tail (ring views)."""
         from . import ops
         g = self.geom
         if g.world == 1:
             ops.fir(self.rf_taps, self.buf, g.decimation, g.rf_outputs, out=self.am, am=True, int8_iq=True)
-            (self.ring.halo if carry_to is None else carry_to).copy_(self.ring.tail)
+            if carry:
+                (self.ring.halo if carry_to is None else carry_to).copy_(self.ring.tail)
         else:
             self.ring.step(self._bulk, self._head)
         ops.fir(self.audio_taps, self.am, g.audio_decimation, g.outputs, out=self.out)

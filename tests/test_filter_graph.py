@@ -556,3 +556,32 @@ def test_fused_fir_am_edge_matches_unfused(graph, orc, elem, T, D):
     y64, bound = orc.fir_f64(taps, x, D, len(outs[True]))
     for fuse in (True, False):
         assert np.all(np.abs(outs[fuse] - np.abs(y64)) <= FIR_TOL * bound + 1e-6 * np.abs(y64) + 1e-30), fuse
+
+
+@pytest.mark.gpu
+def test_device_sink_takes_one_preferred_chunk_per_step(graph, orc):
+    """A DeviceSink (JSON "DeviceSink", preferredBytes) grows its window exactly to the request, as
+    the reference's BaseSink does (BaseSink.cpp:75-77), so every fused Fir -> QuadAmDemod step moves
+    exactly one preferred chunk: 8 192 envelopes (32 KiB, a whole number of allocation granules) per
+    doFilter over ten chunks' worth of buffered outputs (the 2x headroom other sinks take would let
+    the second step run two chunks)."""
+    queue = graph.Queue.named("qds")
+    T, D, per = 255, 4, 8192
+    taps = orc.lowpass_taps(T, 0.1)
+    fir = graph.Node.fir(queue, taps, D, graph.SAMPLE_FLOAT_COMPLEX)
+    am = graph.Node.quad_am_demod(queue)
+    sink = graph.Node.from_json("DeviceSink", '{"commandQueue": "qds", "preferredBytes": %d}' % (4 * per), queue)
+    drv = graph.SteppingDriver()
+    drv.connect(fir, 0, am, 0)
+    drv.connect(am, 0, sink, 0)
+    rng = np.random.default_rng(5)
+    n = 10 * per * D + T - 1
+    fir.push((rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64))
+    left = [fir.output_size()[0] // 8]
+    for _ in range(10):
+        drv.do_filter()
+        left.append(fir.output_size()[0] // 8)
+    queue.sync()
+    assert left[0] == 10 * per
+    assert [left[i] - left[i + 1] for i in range(10)] == [per] * 10
+    assert drv.graph_stats()["fused"] == 10 and am.output_size()[0] == 0

@@ -188,3 +188,29 @@ def test_c5_chain_single_rank_one_launch_matches_split(orc):
     carried, _ = orc.fir_f64(np.abs(orc.lowpass_taps(Ta, 0.02)), (FIR_TOL * (rf_bound + am)).astype(np.float32), Da, n)
     for out in (got, ref):
         assert np.all(np.abs(out - want[:n]) <= carried + FIR_TOL * audio_bound[:n] + 1e-30)
+
+
+def test_c5_ring_views_read_history_in_place(orc):
+    """World 1 with the slots as consecutive views of one input ring (bench.py's C5 layout): slot
+    k + 1's halo IS slot k's segment tail, so step(carry=False) copies nothing, and the audio equals
+    one chain stepping its own buffer with the history copy, bit for bit."""
+    import torch
+    from gpusdr import ops
+    from gpusdr.shard import AmChainShard, ChainShardGeometry
+    T, D, Ta, Da, L = 1023, 10, 255, 20, 40_000
+    dev = torch.device("cuda", 0)
+    geom = ChainShardGeometry(0, 1, L, T, D, Ta, Da)
+    H = geom.halo
+    rf = torch.from_numpy(orc.lowpass_taps(T, 0.04, "blackman")).to(dev)
+    au = torch.from_numpy(orc.lowpass_taps(Ta, 0.02)).to(dev)
+    ring = torch.zeros(2 * (H + 3 * L), dtype=torch.int8, device=dev)
+    views = [AmChainShard(geom, rf, au, dev, buf=ring[2 * k * L: 2 * (k * L + H + L)]) for k in range(3)]
+    ops.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, 0, H + 3 * L, out=ring)  # history + three segments in place
+    one = AmChainShard(geom, rf, au, dev)
+    one.buf[: 2 * H].copy_(ring[: 2 * H])
+    got, ref = [], []
+    for k in range(3):
+        got.append(views[k].step(carry=False).cpu().numpy().copy())
+        one.seg.copy_(views[k].seg)
+        ref.append(one.step().cpu().numpy().copy())
+    assert np.array_equal(np.concatenate(got), np.concatenate(ref))
