@@ -107,9 +107,9 @@ MALL_BYTES = 256 << 20
 class _Slot:
     """One [halo | segment] input buffer, its output, and its halo ring."""
 
-    def __init__(self, g, w, dt, device, ring_cls, stage, incoming):
+    def __init__(self, g, w, dt, device, ring_cls, stage, incoming, buf=None):
         H, L = g.halo, g.seg_len
-        self.buf = torch.zeros(w * (H + L), dtype=dt, device=device)
+        self.buf = torch.zeros(w * (H + L), dtype=dt, device=device) if buf is None else buf
         self.seg = self.buf[w * H:]
         self.ring = ring_cls(g, self.buf[: w * H], self.seg[w * (L - H):], incoming, stage)
         self.bulk_x = self.seg[w * g.bulk_input_offset():]
@@ -133,7 +133,17 @@ class ShardedChain:
         step_bytes = (H + L) * (2 if kind == "i8" else 8) + g.outputs * 4
         self.n_slots = max(1, -(-int(1.5 * MALL_BYTES) // step_bytes))
         incoming = torch.zeros(w * H, dtype=dt, device=device) if (world > 1 and rank == 0) else None
-        self.slots = [_Slot(g, w, dt, device, HaloRing, stage, incoming) for _ in range(self.n_slots)]
+        # one rank: the slots are consecutive views of one input ring when 4 of them fit 20 GB, so
+        # slot k + 1's halo IS slot k's segment tail and only the wrap copies the history (as a live
+        # receiver's input ring holds it; 2^28 cf32 samples: one 8 KB copy per 4 steps, not per step)
+        self.ring = world == 1 and 4 * step_bytes <= 20 * 2**30
+        if self.ring:
+            self.n_slots = max(self.n_slots, 4)
+            ring = torch.zeros(w * (H + self.n_slots * L), dtype=dt, device=device)
+            self.slots = [_Slot(g, w, dt, device, HaloRing, stage, incoming, buf=ring[w * k * L: w * (k * L + H + L)])
+                          for k in range(self.n_slots)]
+        else:
+            self.slots = [_Slot(g, w, dt, device, HaloRing, stage, incoming) for _ in range(self.n_slots)]
         for k, sl in enumerate(self.slots):  # slot k holds the stream position of step k
             if kind == "i8":
                 ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, g.segment_start(k), L, out=sl.seg)
@@ -185,15 +195,18 @@ class ShardedChain:
         else:
             if ev is not None:
                 ev[0].record()
+            # ring views: the next slot's halo already holds this segment's tail (except at the wrap)
+            in_place = self.ring and self.cur != self.n_slots - 1
+            fused_carry = self.kind == "i8" and self.D == 1 and not in_place
             # the fused carry writes the unconsumed tail (T - D samples); with D = 1 that is the
             # whole T - 1 halo in front of the next step's segment
-            if self.kind == "i8" and self.D == 1:
+            if fused_carry:
                 self.ops.fir_am_i8_carry(self.taps, sl.buf, self.D, g.outputs, sl.out, nxt.ring.halo)
             else:
                 self._fir(sl.buf, g.outputs, sl.out)
             if ev is not None:
                 ev[1].record()
-            if not (self.kind == "i8" and self.D == 1):
+            if not in_place and not fused_carry:
                 nxt.ring.halo.copy_(sl.ring.tail)
         self.cur = (self.cur + 1) % self.n_slots
 

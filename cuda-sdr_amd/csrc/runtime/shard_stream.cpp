@@ -1,0 +1,221 @@
+// Time-sharded stream executor (include/gsdr/gsdr_amd.h, gsdrShardStream*): the per-rank step of
+// gpusdr/shard.py's HaloRing protocol for native callers.
+//
+//   buf = [ halo (H = T - 1 samples) | segment (L samples) ]          one per rank, fixed address
+//   step:  event segReady on `stream`; xstream waits for it
+//          exchange(tail = segment[L - H, L) -> next rank, halo <- previous rank) on xstream
+//          bulk:  outputs [head, L/D) over segment + (head D - H)        on `stream`
+//          rank 0: head outputs [0, head) over buf (the halo that arrived last step), then
+//                  `stream` waits for the exchange and copies incoming -> halo for the next step
+//          rank > 0: `stream` waits for the exchange, then the head launch
+// At one rank: a single launch over buf, then the tail is copied into the halo.
+// The FIR is the reference count rule over [halo | segment] (Fir.cpp:178-186): H + L inputs give
+// exactly L / D outputs because L % D == 0.
+#include <gsdr/gsdr_amd.h>
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+
+#include <mutex>
+#include <new>
+
+namespace {
+
+#define SHS_TRY(expr__)                \
+  do {                                 \
+    const hipError_t e__ = (expr__);   \
+    if (e__ != hipSuccess) return e__; \
+  } while (false)
+
+struct DevicePush {
+  int prev = -1;
+  bool ok = true;
+  explicit DevicePush(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DevicePush() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// librccl, loaded on first use so the library itself does not depend on it
+struct Rccl {
+  decltype(&ncclGroupStart) groupStart = nullptr;
+  decltype(&ncclGroupEnd) groupEnd = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  bool ok = false;
+};
+
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (h == nullptr) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (h == nullptr) return;
+    r.groupStart = reinterpret_cast<decltype(&ncclGroupStart)>(dlsym(h, "ncclGroupStart"));
+    r.groupEnd = reinterpret_cast<decltype(&ncclGroupEnd)>(dlsym(h, "ncclGroupEnd"));
+    r.send = reinterpret_cast<decltype(&ncclSend)>(dlsym(h, "ncclSend"));
+    r.recv = reinterpret_cast<decltype(&ncclRecv)>(dlsym(h, "ncclRecv"));
+    r.ok = r.groupStart && r.groupEnd && r.send && r.recv;
+  });
+  return r;
+}
+
+}  // namespace
+
+struct gsdrShardStreamImpl {
+  int32_t device = 0, rank = 0, world = 1;
+  bool int8Iq = false, am = true;
+  size_t T = 0, D = 1, L = 0, H = 0;
+  size_t elem = 8;      // input bytes per sample
+  size_t outElem = 4;   // output bytes per output
+  size_t outputs = 0, head = 0, bulkOffset = 0;
+  float* taps = nullptr;
+  uint8_t* buf = nullptr;
+  uint8_t* incoming = nullptr;
+  hipStream_t xstream = nullptr;
+  hipEvent_t segReady = nullptr, exchanged = nullptr;
+  gsdrHaloExchangeFn exchange = nullptr;
+  void* user = nullptr;
+
+  hipError_t fir(const uint8_t* in, size_t n, uint8_t* out, hipStream_t stream) const {
+    if (n == 0) return hipSuccess;
+    if (int8Iq) {
+      const auto* x = reinterpret_cast<const int8_t*>(in);
+      return am ? gsdrInt8FirFCAmDemod(D, taps, T, x, reinterpret_cast<float*>(out), n, device, stream)
+                : gsdrInt8FirFC(D, taps, T, x, reinterpret_cast<hipFloatComplex*>(out), n, device, stream);
+    }
+    const auto* x = reinterpret_cast<const hipFloatComplex*>(in);
+    return am ? gsdrFirFCAmDemod(D, taps, T, x, reinterpret_cast<float*>(out), n, device, stream)
+              : gsdrFirFC(D, taps, T, x, reinterpret_cast<hipFloatComplex*>(out), n, device, stream);
+  }
+
+  void release() {
+    DevicePush push(device);
+    if (segReady) (void)hipEventDestroy(segReady);
+    if (exchanged) (void)hipEventDestroy(exchanged);
+    if (xstream) (void)hipStreamDestroy(xstream);
+    (void)hipFree(taps);
+    (void)hipFree(buf);
+    (void)hipFree(incoming);
+  }
+};
+
+extern "C" {
+
+GSDR_API hipError_t gsdrShardStreamCreate(int32_t rank, int32_t world, int32_t int8Iq, int32_t am, const float* taps,
+                                          size_t tapCount, size_t decimation, size_t segmentSamples,
+                                          gsdrHaloExchangeFn exchange, void* user, int32_t device,
+                                          gsdrShardStream* streamOut) {
+  if (streamOut == nullptr) return hipErrorInvalidValue;
+  *streamOut = nullptr;
+  if (taps == nullptr || tapCount == 0 || decimation == 0 || world < 1 || rank < 0 || rank >= world)
+    return hipErrorInvalidValue;
+  if (segmentSamples % decimation != 0 || segmentSamples < tapCount - 1 || segmentSamples == 0)
+    return hipErrorInvalidValue;
+  if (world > 1 && exchange == nullptr) return hipErrorInvalidValue;
+  DevicePush push(device);
+  if (!push.ok) return hipErrorInvalidDevice;
+  auto* s = new (std::nothrow) gsdrShardStreamImpl();
+  if (s == nullptr) return hipErrorOutOfMemory;
+  s->device = device;
+  s->rank = rank;
+  s->world = world;
+  s->int8Iq = int8Iq != 0;
+  s->am = am != 0;
+  s->T = tapCount;
+  s->D = decimation;
+  s->L = segmentSamples;
+  s->H = tapCount - 1;
+  s->elem = s->int8Iq ? 2 : 8;
+  s->outElem = s->am ? 4 : 8;
+  s->outputs = s->L / s->D;
+  s->head = (s->H + s->D - 1) / s->D < s->outputs ? (s->H + s->D - 1) / s->D : s->outputs;  // k D < T - 1
+  s->bulkOffset = s->head * s->D - s->H;  // into the segment: the first input of output `head`
+  s->exchange = exchange;
+  s->user = user;
+  hipError_t e = hipMalloc(&s->taps, tapCount * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(s->taps, taps, tapCount * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&s->buf, (s->H + s->L) * s->elem);
+  if (e == hipSuccess) e = hipMemset(s->buf, 0, (s->H + s->L) * s->elem);
+  if (e == hipSuccess && world > 1 && rank == 0 && s->H > 0) {
+    e = hipMalloc(&s->incoming, s->H * s->elem);
+    if (e == hipSuccess) e = hipMemset(s->incoming, 0, s->H * s->elem);
+  }
+  if (e == hipSuccess && world > 1) e = hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking);
+  if (e == hipSuccess && world > 1) e = hipEventCreateWithFlags(&s->segReady, hipEventDisableTiming);
+  if (e == hipSuccess && world > 1) e = hipEventCreateWithFlags(&s->exchanged, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    s->release();
+    delete s;
+    return e;
+  }
+  *streamOut = s;
+  return hipSuccess;
+}
+
+GSDR_API void gsdrShardStreamDestroy(gsdrShardStream s) {
+  if (s == nullptr) return;
+  {
+    DevicePush push(s->device);
+    (void)hipDeviceSynchronize();  // no launch may still read the buffers
+  }
+  s->release();
+  delete s;
+}
+
+GSDR_API void* gsdrShardStreamSegment(gsdrShardStream s) { return s == nullptr ? nullptr : s->buf + s->H * s->elem; }
+
+GSDR_API void* gsdrShardStreamHalo(gsdrShardStream s) { return s == nullptr ? nullptr : s->buf; }
+
+GSDR_API size_t gsdrShardStreamOutputCount(gsdrShardStream s) { return s == nullptr ? 0 : s->outputs; }
+
+GSDR_API hipError_t gsdrShardStreamStep(gsdrShardStream s, void* output, hipStream_t stream) {
+  if (s == nullptr || output == nullptr) return hipErrorInvalidValue;
+  DevicePush push(s->device);
+  if (!push.ok) return hipErrorInvalidDevice;
+  auto* out = static_cast<uint8_t*>(output);
+  uint8_t* tail = s->buf + s->L * s->elem;  // segment[L - H, L) = buf[L, L + H)
+  const size_t haloBytes = s->H * s->elem;
+  if (s->world == 1) {
+    SHS_TRY(s->fir(s->buf, s->outputs, out, stream));
+    if (haloBytes > 0) SHS_TRY(hipMemcpyAsync(s->buf, tail, haloBytes, hipMemcpyDeviceToDevice, stream));
+    return hipSuccess;
+  }
+  uint8_t* dst = s->rank == 0 ? s->incoming : s->buf;
+  const int32_t next = (s->rank + 1) % s->world, prev = (s->rank + s->world - 1) % s->world;
+  SHS_TRY(hipEventRecord(s->segReady, stream));
+  SHS_TRY(hipStreamWaitEvent(s->xstream, s->segReady, 0));
+  if (haloBytes > 0) SHS_TRY(s->exchange(s->user, tail, dst, haloBytes, next, prev, s->xstream));
+  SHS_TRY(hipEventRecord(s->exchanged, s->xstream));
+  SHS_TRY(s->fir(s->buf + (s->H + s->bulkOffset) * s->elem, s->outputs - s->head, out + s->head * s->outElem, stream));
+  if (s->rank == 0) {
+    SHS_TRY(s->fir(s->buf, s->head, out, stream));  // the halo that arrived during the previous step
+    SHS_TRY(hipStreamWaitEvent(stream, s->exchanged, 0));
+    if (haloBytes > 0) SHS_TRY(hipMemcpyAsync(s->buf, s->incoming, haloBytes, hipMemcpyDeviceToDevice, stream));
+  } else {
+    SHS_TRY(hipStreamWaitEvent(stream, s->exchanged, 0));
+    SHS_TRY(s->fir(s->buf, s->head, out, stream));
+  }
+  return hipSuccess;
+}
+
+GSDR_API hipError_t gsdrShardExchangeRccl(void* ncclComm, const void* sendTail, void* recvHalo, size_t bytes,
+                                          int32_t nextRank, int32_t prevRank, hipStream_t xstream) {
+  const Rccl& r = rccl();
+  if (!r.ok) return hipErrorSharedObjectInitFailed;
+  auto comm = static_cast<ncclComm_t>(ncclComm);
+  if (r.groupStart() != ncclSuccess) return hipErrorUnknown;
+  const ncclResult_t a = r.send(sendTail, bytes, ncclUint8, nextRank, comm, xstream);
+  const ncclResult_t b = r.recv(recvHalo, bytes, ncclUint8, prevRank, comm, xstream);
+  const ncclResult_t c = r.groupEnd();
+  return a == ncclSuccess && b == ncclSuccess && c == ncclSuccess ? hipSuccess : hipErrorUnknown;
+}
+
+}  // extern "C"

@@ -108,7 +108,9 @@ GSP_API uint32_t gspDriverDoFilter(gspHandle driver);
 GSP_API uint32_t gspDriverDoFilterGraphed(gspHandle driver, gspHandle queue);
 GSP_API uint32_t gspDriverGraphStats(gspHandle driver, size_t* eager, size_t* captured, size_t* replayed);
 /* Fir -> QuadAmDemod fusion (on by default): a Fir with real taps whose only sink is a QuadAmDemod
- * on the same queue is stepped with it as ONE gsdrFirFCAmDemod launch (bit-identical output).
+ * on the same queue is stepped with it as ONE gsdrFirFCAmDemod launch (the same envelopes within
+ * the FIR tolerance: the fused launch covers a different span, which moves the FFT / matrix-core
+ * kernels' block boundaries and so the last bits of some outputs).
  * gspDriverFusedSteps counts the fused edge moves. */
 GSP_API uint32_t gspDriverSetFuseFirAm(gspHandle driver, int32_t on);
 GSP_API uint32_t gspDriverFusedSteps(gspHandle driver, size_t* fused);

@@ -241,6 +241,52 @@ GSDR_API size_t gsdrAmChainGraphCaptures(gsdrAmChain chain);
 /* Forget all history: the next step is a first step again. */
 GSDR_API hipError_t gsdrAmChainReset(gsdrAmChain chain);
 
+/*
+ * Time-sharded stream (the native form of gpusdr/shard.py's HaloRing, for C /
+ * C++ callers): one executor per rank. In step s, rank g of G owns stream samples
+ * [(s G + g) L, (s G + g + 1) L) and filters [halo | segment], the halo being the T - 1 samples in
+ * front of the segment: rank g - 1's tail of the same step, or, for rank 0, rank G - 1's tail of the
+ * previous step (zeros before the first step unless primed through gsdrShardStreamHalo). Outputs
+ * L / D per step, the stream's outputs from index (s G + g) L / D on, exactly as one FIR over the
+ * whole stream fed T - 1 zeros first (Fir.cpp:178-186 count rule). At G = 1 the halo is the rank's
+ * own previous tail (one launch over [halo | segment] plus a T - 1 sample copy).
+ *
+ * A step enqueues on `stream`: the bulk launch (outputs whose windows lie in the segment) while the
+ * caller's exchange moves the tail to rank g + 1 and the halo from rank g - 1 on the executor's
+ * second stream, then the head launch (outputs that read the halo; rank 0 uses the halo received
+ * one step earlier and never waits). The exchange is the caller's transport:
+ *   exchange(user, sendTail, recvHalo, bytes, nextRank, prevRank, xstream) enqueues on (or performs
+ *   before returning, ordered after earlier work on) `xstream` the send of `bytes` device bytes at
+ *   sendTail to nextRank and the receive of `bytes` from prevRank into recvHalo (device).
+ * gsdrShardExchangeRccl is such a hook over an RCCL communicator (user = the ncclComm_t; librccl is
+ * loaded on first use, one GPU per rank).
+ *
+ * input: int8Iq != 0 -> interleaved int8 IQ (2 bytes per sample), else cf32; output: am != 0 -> the
+ * AM envelope (float), else cf32 FIR outputs. L must be a multiple of D and >= T - 1; taps are host
+ * memory (copied).
+ */
+typedef struct gsdrShardStreamImpl* gsdrShardStream;
+typedef hipError_t (*gsdrHaloExchangeFn)(void* user, const void* sendTail, void* recvHalo, size_t bytes,
+                                         int32_t nextRank, int32_t prevRank, hipStream_t xstream);
+GSDR_API hipError_t gsdrShardStreamCreate(int32_t rank, int32_t world, int32_t int8Iq, int32_t am,
+                                          const float* taps, size_t tapCount, size_t decimation, size_t segmentSamples,
+                                          gsdrHaloExchangeFn exchange, void* user, int32_t device,
+                                          gsdrShardStream* streamOut);
+GSDR_API void gsdrShardStreamDestroy(gsdrShardStream s);
+/* Device address of the segment (segmentSamples samples) the next step filters: write the next
+ * segment there (ordered before the step on its stream). */
+GSDR_API void* gsdrShardStreamSegment(gsdrShardStream s);
+/* Device address of the halo (tapCount - 1 samples in front of the segment), e.g. to prime the
+ * first step with the stream's preceding samples. */
+GSDR_API void* gsdrShardStreamHalo(gsdrShardStream s);
+/* Outputs per step: segmentSamples / decimation. */
+GSDR_API size_t gsdrShardStreamOutputCount(gsdrShardStream s);
+/* One step; `output` (device) receives gsdrShardStreamOutputCount outputs. Asynchronous on
+ * `stream`; the next segment may be written on `stream` after it returns. */
+GSDR_API hipError_t gsdrShardStreamStep(gsdrShardStream s, void* output, hipStream_t stream);
+GSDR_API hipError_t gsdrShardExchangeRccl(void* ncclComm, const void* sendTail, void* recvHalo, size_t bytes,
+                                          int32_t nextRank, int32_t prevRank, hipStream_t xstream);
+
 #ifdef __cplusplus
 }
 #endif

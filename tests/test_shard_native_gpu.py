@@ -1,0 +1,109 @@
+"""The native time-sharded stream executor (gsdrShardStream*, gpusdr/native_shard.py): the halo-ring
+step of gpusdr/shard.py in C++, its exchange supplied by the caller. 1, 2 and 4 ranks (gloo ranks on
+cuda:0, the halo staged through host memory by a Python exchange hook) with the real gfx950 FIR
+kernels - cf32 on the FFT kernel (C4's 1023 taps, D = 1; C3's D = 10) and int8 IQ with AM on the
+matrix-core kernel - must reproduce the float64 oracle over the whole primed stream within the FIR
+tolerance 1e-6 * sum|h||x|, the same bar as tests/test_shard_gpu.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIR_TOL = 1e-6
+STEPS = 3
+CASES = {  # name: (int8 IQ, AM, taps, D, segment samples)
+    "c4": (False, False, 1023, 1, 20_000),
+    "c3": (False, True, 1023, 10, 30_000),
+    "i8": (True, True, 255, 4, 16_000),
+}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _stream_piece(ops, torch, i8, start, n, dev):
+    """Samples [start, start + n) of the test stream, generated on the GPU."""
+    if i8:
+        x = torch.empty(2 * n, dtype=torch.int8, device=dev)
+        ops.synth_iq_int8(0x5EED, 1e9, 1e3, 7.5e7, start, n, out=x)
+    else:
+        x = torch.empty(n, dtype=torch.complex64, device=dev)
+        ops.synth_wideband_cf32(0xC4, 0.013, 0.31, start, n, out=x)
+    return x
+
+
+def _rank_main(rank, world, port, case, out_dir):
+    import sys
+    sys.path[:0] = [os.path.join(REPO, "cuda-sdr_amd"), os.path.join(REPO, "oracle")]
+    import torch
+    import torch.distributed as dist
+
+    import oracle as orc
+    from gpusdr import ops
+    from gpusdr.native_shard import ShardStream, host_staged_exchange
+
+    i8, am, T, D, L = CASES[case]
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    ops.set_ws_spin_limit(1 << 28)  # several ranks time-share the GPU
+    ops.ws_aborts(reset=True)
+    taps = orc.lowpass_taps(T, 0.04, "blackman")
+    sh = ShardStream(rank, world, taps, D, L, int8_iq=i8, am=am,
+                     exchange=host_staged_exchange() if world > 1 else None)
+    H = T - 1
+    if rank == 0:  # the stream's first H samples are the primed history of rank 0's first step
+        sh.write_halo(_stream_piece(ops, torch, i8, 0, H, dev))
+    outs = []
+    for step in range(STEPS):
+        start = H + (step * world + rank) * L
+        sh.write_segment(_stream_piece(ops, torch, i8, start, L, dev))
+        y = sh.step()
+        torch.cuda.synchronize()
+        outs.append(y.cpu().numpy().copy())
+    aborts = ops.ws_aborts(reset=True)
+    if aborts:
+        raise RuntimeError(f"rank {rank}: {aborts} wave-specialised hand-off aborts")
+    sh.close()
+    np.save(os.path.join(out_dir, f"{case}_rank{rank}.npy"), np.stack(outs))
+    if rank == 0:  # the whole stream as the GPU generates it, for the oracle
+        full = _stream_piece(ops, torch, i8, 0, H + world * STEPS * L, dev)
+        np.save(os.path.join(out_dir, f"{case}_stream.npy"), full.cpu().numpy())
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,world", [("c4", 1), ("c4", 2), ("c4", 4), ("c3", 2), ("i8", 1), ("i8", 2)])
+def test_native_shard_stream_matches_oracle(tmp_path, orc, case, world):
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_main, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    i8, am, T, D, L = CASES[case]
+    per = [np.load(os.path.join(tmp_path, f"{case}_rank{r}.npy")) for r in range(world)]
+    got = np.concatenate([per[r][s] for s in range(STEPS) for r in range(world)])
+    stream = np.load(os.path.join(tmp_path, f"{case}_stream.npy"))
+    x = orc.int8_to_float(stream).view(np.complex64) if i8 else stream
+    n = world * STEPS * L // D
+    assert len(got) == n
+    y64, bound = orc.fir_f64(orc.lowpass_taps(T, 0.04, "blackman"), x, D, n)
+    want = np.abs(y64) if am else y64
+    err = np.abs(got.astype(np.complex128) - want)
+    assert np.all(err <= FIR_TOL * bound + 1e-30), float(np.max(err / (bound + 1e-30)))
+
+
+def test_native_shard_stream_rejects_bad_shapes():
+    from gpusdr.native_shard import ShardStream
+    with pytest.raises(RuntimeError):
+        ShardStream(0, 1, np.ones(8, np.float32), 3, 1000)  # L not a multiple of D
+    with pytest.raises(RuntimeError):
+        ShardStream(0, 2, np.ones(8, np.float32), 1, 1000)  # two ranks need an exchange
