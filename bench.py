@@ -151,6 +151,10 @@ class ShardedChain:
                 ops.synth_wideband_cf32(0xC3, 0.013, 0.31, g.segment_start(k), L, out=sl.seg)
         self.cur = 0
         self.ev = None
+        if world == 1:  # the step's launch per slot, validated once (a C2 launch is ~36 us: the
+            # argument checks of ops.fir on every step would leave the GPU waiting for the host)
+            for sl in self.slots:
+                sl.launch = ops.bind_fir(self.taps, sl.buf, D, g.outputs, sl.out, am=True, int8_iq=(kind == "i8"))
 
     @property
     def slot(self):
@@ -203,7 +207,7 @@ class ShardedChain:
             if fused_carry:
                 self.ops.fir_am_i8_carry(self.taps, sl.buf, self.D, g.outputs, sl.out, nxt.ring.halo)
             else:
-                self._fir(sl.buf, g.outputs, sl.out)
+                sl.launch()
             if ev is not None:
                 ev[1].record()
             if not in_place and not fused_carry:

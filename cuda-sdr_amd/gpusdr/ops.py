@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from ._native import check, lib
+from ._native import HipError, check, lib
 
 
 def _stream(t: torch.Tensor):
@@ -103,6 +103,40 @@ def fir(taps: torch.Tensor, x: torch.Tensor, decimation: int = 1, num_outputs: i
     fn = getattr(lib(), _FIR_ENTRY[key])
     check(fn(d, taps.data_ptr(), T, x.data_ptr(), out.data_ptr(), num_outputs, _dev(x), _stream(x)), fn.__name__)
     return out
+
+
+def bind_fir(taps: torch.Tensor, x: torch.Tensor, decimation: int, num_outputs: int, out: torch.Tensor,
+             am: bool = False, int8_iq: bool = False):
+    """The launch `fir(taps, x, decimation, num_outputs, out=out, am=am, int8_iq=int8_iq)` validated
+    once and bound to fixed addresses and torch's current stream: returns a zero-argument callable
+    that only enqueues the kernel (a few microseconds of host time instead of the argument checks -
+    what a step loop over fixed buffers needs when the kernel itself takes tens of microseconds)."""
+    taps_c = taps.dtype == torch.complex64
+    _require(taps, torch.complex64 if taps_c else torch.float32, "taps")
+    kind = "i8iq" if int8_iq else ("c64" if x.dtype == torch.complex64 else "f32")
+    _require(x, {"i8iq": torch.int8, "c64": torch.complex64, "f32": torch.float32}[kind], "x")
+    key = (taps_c, kind, am)
+    if key not in _FIR_ENTRY:
+        raise ValueError(f"unsupported FIR combination {key}")
+    d, T = max(1, int(decimation)), taps.numel()
+    n_in = x.numel() // 2 if int8_iq else x.numel()
+    if num_outputs > 0 and (num_outputs - 1) * d + T > n_in:
+        raise ValueError("input too short for the requested outputs")
+    out_dtype = torch.float32 if (am or (not taps_c and kind == "f32")) else torch.complex64
+    _require(out, out_dtype, "out")
+    if out.numel() < num_outputs:
+        raise ValueError("out too small")
+    fn = getattr(lib(), _FIR_ENTRY[key])
+    args = (d, taps.data_ptr(), T, x.data_ptr(), out.data_ptr(), int(num_outputs), _dev(x), _stream(x))
+    name = fn.__name__
+    keep = (taps, x, out)  # the bound addresses stay valid while the callable lives
+
+    def launch():
+        if num_outputs > 0:
+            code = fn(*args)
+            if code != 0:
+                raise HipError(f"{name} failed with hipError_t {code} ({len(keep)} bound tensors)")
+    return launch
 
 
 def fir_am_i8_carry(taps: torch.Tensor, iq: torch.Tensor, decimation: int, num_outputs: int,

@@ -764,3 +764,28 @@ def test_mixed_long_filter_runs_on_fft_kernel(ops, orc, kind):
     for yy, aa, what in ((y, am, "fft"), (y_dir, am_dir, "direct")):
         _check_fir(yy, y64, bound, ("mixed", kind, what))
         assert np.all(np.abs(aa - np.abs(y64)) <= FIR_TOL * bound + 1e-30), what
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i8", [False, True])
+def test_bound_fir_launch_matches_fir(orc, i8):
+    """ops.bind_fir (the bench's pre-validated launch) enqueues exactly ops.fir's kernel: bit-equal
+    outputs, and it rejects an input too short for the outputs at bind time."""
+    import torch
+    from gpusdr import ops
+    dev = torch.device("cuda", 0)
+    T, D, n = 127, 1 if i8 else 10, 5000
+    taps = torch.from_numpy(orc.lowpass_taps(T, 0.1)).to(dev)
+    n_in = (n - 1) * D + T
+    if i8:
+        x = torch.randint(-128, 128, (2 * n_in,), dtype=torch.int8, device=dev)
+    else:
+        x = torch.randn(n_in, dtype=torch.complex64, device=dev)
+    a = torch.empty(n, dtype=torch.float32, device=dev)
+    b = torch.empty(n, dtype=torch.float32, device=dev)
+    ops.fir(taps, x, D, n, out=a, am=True, int8_iq=i8)
+    ops.bind_fir(taps, x, D, n, b, am=True, int8_iq=i8)()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    with pytest.raises(ValueError):
+        ops.bind_fir(taps, x[: x.numel() // 2], D, n, b, am=True, int8_iq=i8)
