@@ -276,3 +276,23 @@ def test_full_c2_and_c5_sizes(ops, orc):
         want, audio_bound = orc.fir_f64(au, a.astype(np.float32), Da, 1)
         carried, _ = orc.fir_f64(np.abs(au), (FIR_TOL * (rf_bound + a)).astype(np.float32), Da, 1)
         assert abs(got[r] - want[0]) <= carried[0] + FIR_TOL * audio_bound[0] + 1e-30, k
+
+
+@pytest.mark.parametrize("am", [True, False])
+def test_fft_fir_d1_unaligned_output(ops, orc, am):
+    """The D = 1 kernel stores a row's eight phases as 16-byte units only when `out` is 16-byte
+    aligned; at an offset of one output it falls back to per-output stores: same values, nothing
+    written outside the requested outputs."""
+    import torch
+    T, D, n_out = 1023, 1, 7001
+    n_in = (n_out - 1) * D + T
+    x = _signal("c64", n_in, T + D, orc)
+    taps = orc.lowpass_taps(T, 0.02).astype(np.float32)
+    x_d, taps_d = _dev(x), _dev(taps)
+    dt = torch.float32 if am else torch.complex64
+    ref = ops.fir(taps_d, x_d, D, n_out, am=am)
+    buf = torch.full((n_out + 2,), 7.0, dtype=dt, device=x_d.device)
+    ops.fir(taps_d, x_d, D, n_out, out=buf[1:n_out + 1], am=am)
+    got = _host(buf)
+    assert got[0] == 7.0 and got[-1] == 7.0
+    assert np.array_equal(got[1:n_out + 1], _host(ref))
