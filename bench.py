@@ -695,7 +695,7 @@ def main():
     ap.add_argument("--share-gpu", action="store_true",
                     help="run every rank on cuda:0 (testing the multi-rank path on a one-GPU box; gloo)")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the secondary measurements (C4 strong scaling, C5, the C3 node path) that the "
+                    help="skip the secondary measurements (C4 strong scaling, C5, C2, the C3 node path) that the "
                          "default run adds to its JSON line under 'extras'")
     args = ap.parse_args()
     if args.share_gpu and args.backend != "gloo":
@@ -724,7 +724,8 @@ def main():
 
     # secondary workloads in the same run, so the driver's 1/2/4/8-GPU runs measure every config
     # BASELINE.json names: C4 as stated (one 2^30-sample stream split over the GPUs, strong scaling),
-    # the C5 chain, and (N = 1) C3 through the reference's node API
+    # the C5 chain, C2 (configs[1], the HackRF-shaped int8 chain), and (N = 1) C3 through the
+    # reference's node API
     extras = {}
     if args.workload == "c3" and not args.no_extras:
         if world == 1:
@@ -733,7 +734,7 @@ def main():
                       getattr(chain, "n_slots", 1))
         del chain
         torch.cuda.empty_cache()
-        for wl, k, w in (("c4s", 6, 2), ("c5", 20, 3)):
+        for wl, k, w in (("c4s", 6, 2), ("c5", 20, 3), ("c2", 50, 5)):
             xc = (AmChainSharded(ops, rank, world, device, stage) if wl == "c5" else
                   ShardedChain(ops, wl, rank, world, device, stage))
             e2, k2, _ = timed_steps(xc, k, w, world, args.backend, device, local, ops)

@@ -145,6 +145,16 @@ class ChainShardGeometry:
         return (self.rank - 1) % self.world
 
 
+def _bytes(t):
+    """The same storage as a flat uint8 tensor (a contiguous halo region)."""
+    import torch
+    if t.dtype == torch.uint8:
+        return t
+    if not t.is_contiguous():
+        raise ValueError("halo buffers must be contiguous")
+    return t.reshape(-1).view(torch.uint8)
+
+
 class HaloRing:
     """Per-rank halo state and the per-step protocol.
 
@@ -173,6 +183,10 @@ class HaloRing:
         if self.stage:
             self._send.copy_(self.tail)  # synchronous: the tail is final once this returns
             send, recv = self._send, self._recv
+        # byte views: the halo is opaque samples, and ProcessGroupNCCL's send/recv have no complex
+        # datatype ("Unconvertible NCCL type" for complex64; its collectives view complex as real,
+        # its point-to-point ops do not)
+        send, recv = _bytes(send), _bytes(recv)
         return dist.batch_isend_irecv([dist.P2POp(dist.isend, send, g.next_rank),
                                        dist.P2POp(dist.irecv, recv, g.prev_rank)])
 
