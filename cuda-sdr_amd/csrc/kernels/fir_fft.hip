@@ -458,6 +458,11 @@ __device__ __forceinline__ void transposeRows(Rows<D, kCf32>& R, f2* s, int l) {
   }
 }
 
+// Row groups loaded non-temporal (bit j: group j), see loadRows.
+#ifndef GSDR_FFT_NT_GROUPS
+#define GSDR_FFT_NT_GROUPS 0x3C
+#endif
+
 // Load block b (rows b V .. b V + 511) and transpose to rows. Loads past the input's end read 0.
 template <int D>
 __device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kCf32>& R, f2* s, int l) {
@@ -475,8 +480,8 @@ __device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kCf32
       // (the previous block's tail) and 6-7 (re-read by the next block) keep the default policy so
       // the overlap stays an L2 hit. C3 490 -> 485 us, profiles/r03/exp/fft_nt_mid_ab.log
       const int off = ((j * D / 2 + i) * 64 + l) * 16;
-      const f4 u = (j >= 2 && j <= 5) ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2))
-                                      : __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      const f4 u = ((GSDR_FFT_NT_GROUPS >> j) & 1) ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2))
+                                                   : __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       R.v[j][2 * i] = f2{u.x, u.y};
       R.v[j][2 * i + 1] = f2{u.z, u.w};
     }

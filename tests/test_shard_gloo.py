@@ -123,3 +123,19 @@ def test_geometry_rules():
     assert g.next_rank == 3 and g.prev_rank == 1
     with pytest.raises(ValueError):
         ShardGeometry(0, 2, 1001, 31, 10)
+
+
+def test_halo_byte_views():
+    """The ring hands halos to torch.distributed as uint8 views of the same storage:
+    ProcessGroupNCCL's send/recv have no complex datatype ("Unconvertible NCCL type")."""
+    import torch
+    from gpusdr.shard import _bytes
+    x = torch.arange(12, dtype=torch.float32).to(torch.complex64)
+    b = _bytes(x[3:7])
+    assert b.dtype == torch.uint8 and b.numel() == 4 * 8
+    b.zero_()  # same storage
+    assert torch.all(x[3:7] == 0) and x[2] == 2 and x[7] == 7
+    i8 = torch.arange(20, dtype=torch.int8)
+    assert _bytes(i8[4:]).numel() == 16
+    with pytest.raises(ValueError):
+        _bytes(torch.zeros(4, 4, dtype=torch.complex64)[:, 1])
