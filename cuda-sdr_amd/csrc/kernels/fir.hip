@@ -527,11 +527,18 @@ __global__ __launch_bounds__(kThreads) void firSmallKernel(FirArgs a) {
 // registers: 2 window reads per 8 packed FMAs (firSmallKernel: 2 LDS reads per FMA).
 // Sum order: per phase, ceil(T / D) taps in sequence; then the phase partials in order (the
 // same bound as firSmallKernel's; tests hold both against float64).
-constexpr int kDecR = 4;
-constexpr int kDecThreads = 128;
+#ifndef GSDR_DEC_R
+#define GSDR_DEC_R 4
+#endif
+#ifndef GSDR_DEC_THREADS
+#define GSDR_DEC_THREADS 128
+#endif
+constexpr int kDecR = GSDR_DEC_R;
+constexpr int kDecThreads = GSDR_DEC_THREADS;
 constexpr int kDecOut = kDecR * kDecThreads;
-constexpr int kDecLoads = 24;  // float4 staging loads in flight per lane: one HBM round trip per
-                               // block at C5's shape (2620 float4 per block), small launches are latency-bound
+// float4 staging loads in flight per lane: one HBM round trip per block at C5's shape (2620 float4
+// per 512-output block); small launches are latency-bound
+constexpr int kDecLoads = (24 * 128 * kDecOut / 512 + kDecThreads - 1) / kDecThreads;
 constexpr int kDecMaxQ = 32;   // taps per phase
 
 // Per-phase-pair LDS: the window rows (even count: 16 B aligned rows) and the tap pairs (even count)
