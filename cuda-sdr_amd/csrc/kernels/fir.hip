@@ -934,6 +934,33 @@ hipError_t gsdrInt8FirFCAmDemod(size_t decimation, const float* taps, size_t tap
                                             stream);
 }
 
+hipError_t gsdrInt8FirFCAmDemodFirFF(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
+                                    size_t rfCount, float* amWindow, size_t amHistory, int storeAm,
+                                    size_t audioDecimation, const float* audioTaps, size_t audioTapCount,
+                                    float* audioOut, size_t audioCount, int32_t device, hipStream_t stream) {
+  if (rfCount == 0 && audioCount == 0) return hipSuccess;
+  const size_t da = audioDecimation < 1 ? 1 : audioDecimation;
+  if (amWindow == nullptr || (rfCount > 0 && (inputIq == nullptr || taps == nullptr || tapCount == 0)) ||
+      (audioCount > 0 && (audioTaps == nullptr || audioOut == nullptr || audioTapCount == 0)))
+    return hipErrorInvalidValue;
+  if (audioCount > 0 && (audioCount - 1) * da + audioTapCount > amHistory + rfCount) return hipErrorInvalidValue;
+  float* amOut = amWindow + amHistory;
+  if (rfCount > 0 && audioCount > 0) {
+    DevicePush push(device);
+    if (!push.ok) return hipErrorInvalidDevice;
+    const hipError_t e = launchFirI8DecMfmaAudio(inputIq, taps, tapCount, decimation, storeAm ? amOut : nullptr,
+                                                 rfCount, amWindow, amHistory, audioTaps, audioTapCount, da,
+                                                 audioOut, audioCount, stream);
+    if (e != hipErrorNotSupported) return e;
+  }
+  // the two stages (amWindow's new part doubles as the intermediate)
+  hipError_t e = launchFir<kFirFC, kInI8IQ, kEpiAm>(inputIq, taps, tapCount, decimation, amOut, rfCount, device,
+                                                    stream);
+  if (e != hipSuccess) return e;
+  return launchFir<kFirFF, kInF32, kEpiPair>(amWindow, audioTaps, audioTapCount, da, audioOut, audioCount, device,
+                                             stream);
+}
+
 hipError_t gsdrInt8FirFCAmDemodCarry(size_t decimation, const float* taps, size_t tapCount, const int8_t* inputIq,
                                      float* output, size_t outputCount, int8_t* carryIq, int32_t device,
                                      hipStream_t stream) {

@@ -637,6 +637,11 @@ constexpr int kWsPThreads = kWsProducers * kWave;           // 256
 constexpr int kWsThreads = kCfThreads + kWsPThreads;        // 768
 constexpr int kWsDirect = 0x7fffffff;                       // plane-set mode: direct fp32 tile
 constexpr int kWsSpinLimit = 1 << 22;                       // default s_sleep(1) iterations (~0.1 s)
+// Fused audio stage (firI8WsKernel<.., AUD>): AM ring of kAmRing tiles in LDS; the producers compute
+// the audio outputs of tile i - kAudioLag after producing the planes of tile i.
+constexpr int kAmRing = 8;
+constexpr int kAudioLag = 3;
+constexpr int kAudioMaxTaps = 256;  // 4 taps per lane
 
 struct WsCtl {
   int planesFull[2];
@@ -645,6 +650,8 @@ struct WsCtl {
   int partsFree[2];
   int pstat;
   int tapsRead;                       // consumer waves done reading the taps staged in `part`
+  int amFull;                         // fused audio stage: consumer waves' AM of a tile in the ring
+  int amFree;                         // producer waves done with the audio outputs of a tile
   int abort;
   int mode[2];                        // per plane set: scale exponent sx, or kWsDirect
   float stat[2][2][kWsProducers];     // [tile parity][max, smallest block max][producer wave]
@@ -835,9 +842,9 @@ __device__ __forceinline__ void wsProducerTile(const CfFirArgs& a, int Wl, int8_
 // local tile index (its partials: buffer j & 1 when double-buffered, else the single buffer),
 // waited for until every wave has written them. `mode`: the tile's scale exponent, or kWsDirect
 // (outputs already stored).
-template <int EPI, bool I8>
+template <int EPI, bool I8, bool AUD = false>
 __device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* part, WsCtl* c, int sh, int tile, int j,
-                                             bool dbp, int mode, int tid) {
+                                             bool dbp, int mode, int tid, float* ring = nullptr, bool lead = false) {
   const int lane = tid & (kWave - 1);
   const int wave = tid >> 6;
   const int b = dbp ? (j & 1) : 0;
@@ -853,7 +860,15 @@ __device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* pa
     wsSignal(&c->partsFree[b], lane);
     const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * (lane >> 5);
     const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + (lane & 31);
-    if (k < a.nOut) {
+    if constexpr (AUD) {  // int8, AM: the tile's AM samples into the ring for the producers' audio FIR
+      const float v = __builtin_amdgcn_sqrtf(fmaf(yi, yi, yq * yq)) * ldexpf(1.0f / 127.0f, -sh);
+      // slot j mod kAmRing is free once the producers finished the audio outputs of tile j - kAmRing + 1
+      if (j - kAmRing + 2 > 0) wsWait(c, &c->amFree, kWsProducers * (j - kAmRing + 2));
+      ring[(j & (kAmRing - 1)) * kCfTileOut + 32 * orow + (lane & 31)] = k < a.nOut ? v : 0.0f;
+      wsSignal(&c->amFull, lane);
+      // the lead tile belongs to the previous block (computed here only for the audio windows)
+      if (a.out != nullptr && k < a.nOut && !(lead && j == 0)) reinterpret_cast<float*>(a.out)[k] = v;
+    } else if (k < a.nOut) {
       if (I8) {  // the epilogue of firI8DecMfmaKernel: y = acc 2^-sc / 127
         const float outScale = ldexpf(1.0f / 127.0f, -sh);
         if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = __builtin_amdgcn_sqrtf(fmaf(yi, yi, yq * yq)) * outScale;
@@ -872,9 +887,9 @@ __device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* pa
 // Consumer waves of the wave-specialised kernels (cf32: 4 planes per set, 3 products; int8 IQ:
 // 2 planes, 2 products, no direct tiles). `part` first holds the staged taps (consumers turn them
 // into B fragments), then the partial accumulators.
-template <int KS, int EPI, bool I8>
+template <int KS, int EPI, bool I8, bool AUD = false>
 __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, float* part, WsCtl* c, int sh, int t0,
-                                            int n, int tid, bool dbp) {
+                                            int n, int tid, bool dbp, float* ring = nullptr, bool lead = false) {
   constexpr int NP = I8 ? 2 : 4;
   const int lane = tid & (kWave - 1);
   const int wave = waveUniform(tid >> 6);
@@ -918,11 +933,11 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
       // the partial hand-off counters advance as for any tile (the count-based waits rely on it)
       if (dbp) {
         wsSignal(&c->partsFull[i & 1], lane);
-        if (i >= 1) wsReduceTile<EPI, I8>(a, part, c, sh, tile - 1, i - 1, true, prevMode, tid);
+        if (i >= 1) wsReduceTile<EPI, I8, AUD>(a, part, c, sh, tile - 1, i - 1, true, prevMode, tid, ring, lead);
       } else {
         wsWait(c, &c->partsFree[0], kCfWaves * i);
         wsSignal(&c->partsFull[0], lane);
-        wsReduceTile<EPI, I8>(a, part, c, sh, tile, i, false, mode, tid);
+        wsReduceTile<EPI, I8, AUD>(a, part, c, sh, tile, i, false, mode, tid, ring, lead);
       }
       prevMode = mode;
       continue;
@@ -967,18 +982,18 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
 #pragma unroll
       for (int k = 0; k < 16; ++k) pb[(wave * 16 + k) * kWave + lane] = acc[k];
       wsSignal(&c->partsFull[b], lane);
-      if (i >= 1) wsReduceTile<EPI, I8>(a, part, c, sh, tile - 1, i - 1, true, prevMode, tid);
+      if (i >= 1) wsReduceTile<EPI, I8, AUD>(a, part, c, sh, tile - 1, i - 1, true, prevMode, tid, ring, lead);
     } else {
       wsWait(c, &c->partsFree[0], kCfWaves * i);  // every wave has read tile i - 1's partials
       if (i == 0) wsWait(c, &c->tapsRead, kCfWaves);
 #pragma unroll
       for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
       wsSignal(&c->partsFull[0], lane);
-      wsReduceTile<EPI, I8>(a, part, c, sh, tile, i, false, mode, tid);
+      wsReduceTile<EPI, I8, AUD>(a, part, c, sh, tile, i, false, mode, tid, ring, lead);
     }
     prevMode = mode;
   }
-  if (dbp && n >= 1) wsReduceTile<EPI, I8>(a, part, c, sh, t0 + n - 1, n - 1, true, prevMode, tid);
+  if (dbp && n >= 1) wsReduceTile<EPI, I8, AUD>(a, part, c, sh, t0 + n - 1, n - 1, true, prevMode, tid, ring, lead);
 }
 
 template <int KS, int G, int EPI>
@@ -1072,6 +1087,15 @@ struct I8DecArgs {
   int32_t dbp;          // wave-specialised kernel: two partial-sum buffers
   int32_t spinLimit;    // as CfFirArgs
   uint32_t* abortOut;
+  // fused audio stage (firI8WsKernel<.., true>): audio[j] = sum_t aTaps[t] A(j aD - amH + t) for
+  // j < aN, where A(k) is AM output k of this launch (k >= 0) or amHist[amH + k] (k < 0)
+  const float* aTaps;
+  float* aOut;
+  const float* amHist;
+  int64_t aN;
+  int32_t aT;
+  int32_t aD;
+  int32_t amH;
 };
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -1301,7 +1325,62 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
   wsSignal(&c->planesFull[set], lane);
 }
 
-template <int KS, int G, int EPI>
+// Fused audio stage, producer side: the audio outputs of block-local tile t (global tile t0 + t) -
+// those whose window ends in that tile's AM range (tile 0 of the launch: also windows ending
+// before AM sample 0, in the history) - from the AM ring the consumers fill (tiles t - 1 and t are
+// in it: a window spans at most 256 AM samples), then amFree. Wave pw takes outputs jLo + pw + 4 b;
+// lane l accumulates taps l + 64 m (m < 4, conflict-free ring reads), then a wave sum per output.
+// The lead tile (the previous block's last, computed for the ring only) has no outputs here.
+__device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* ring, WsCtl* c, int t0, bool lead, int t,
+                                            int ptid, const float (&ht)[4]) {
+  const int lane = ptid & (kWave - 1);
+  const int pw = ptid >> 6;
+  if (!(lead && t == 0)) {
+    wsWait(c, &c->amFull, kCfWaves * (t + 1));
+    const int64_t g = (int64_t)(t0 + t);
+    // smallest j whose window end j aD - amH + aT - 1 is >= X
+    auto firstJ = [&](int64_t X) -> int64_t {
+      const int64_t num = X + a.amH - a.aT + 1;
+      return num <= 0 ? 0 : (num + a.aD - 1) / a.aD;
+    };
+    const int64_t jLo = g == 0 ? 0 : firstJ(g * kCfTileOut);
+    int64_t jHi = firstJ((g + 1) * kCfTileOut);
+    if (jHi > a.aN) jHi = a.aN;
+    for (int64_t jb = jLo + pw; jb < jHi; jb += 8 * kWsProducers) {
+      float s[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        s[b] = 0.0f;
+        const int64_t j = jb + kWsProducers * b;
+        if (j < jHi) {  // wave-uniform
+          const int64_t k0 = j * a.aD - a.amH;  // the window's first AM sample
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int tp = lane + kWave * m;
+            const int64_t k = k0 + tp;
+            if (tp < a.aT) {
+              const float x = k >= 0 ? ring[(((int)(k >> 9) - t0) & (kAmRing - 1)) * kCfTileOut + (int)(k & 511)]
+                                     : a.amHist[a.amH + k];
+              s[b] = fmaf(ht[m], x, s[b]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < 8; ++b) s[b] = waveSum(s[b]);
+      if (lane == 0) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const int64_t j = jb + kWsProducers * b;
+          if (j < jHi) a.aOut[j] = s[b];
+        }
+      }
+    }
+  }
+  wsSignal(&c->amFree, lane);
+}
+
+template <int KS, int G, int EPI, bool AUD = false>
 __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int Wl) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   float* part = reinterpret_cast<float*>(smem + 4 * a8.planeStride);
@@ -1315,9 +1394,18 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
   const int D = a8.D, T = a8.T;
 
   const int q = a8.tiles / (int)gridDim.x, r = a8.tiles % (int)gridDim.x;
-  const int t0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
-  const int n = q + ((int)blockIdx.x < r ? 1 : 0);
+  int t0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
+  int n = q + ((int)blockIdx.x < r ? 1 : 0);
   if (n <= 0) return;
+  // fused audio: every block but the first also computes the tile before its range (the lead) into
+  // its AM ring, so each audio window it owns is complete on chip (+1 tile in ~100 at C5's size)
+  bool lead = false;
+  if (AUD && t0 > 0) {
+    --t0;
+    ++n;
+    lead = true;
+  }
+  float* ring = AUD ? reinterpret_cast<float*>(smem + 4 * a8.planeStride + 2 * kCfPartialBytes) : nullptr;
 
   // ---- taps -> LDS (zero-padded to [-31 D, 128 KS)), block max; zero both plane sets --------
   if (tid < kWsCtlZeroWords) reinterpret_cast<int*>(c)[tid] = 0;
@@ -1352,12 +1440,24 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
     const i4v r1 = wsI8TileRsrc(a8, t0 + 1, n > 1);
 #pragma unroll
     for (int j = 0; j < G; ++j) wsI8LoadGroup<G>(r1, Wl, ptid, j, wB);
+    float ht[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // audio taps lane + 64 m
+    if constexpr (AUD) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int tp = lane + kWave * m;
+        ht[m] = tp < a8.aT ? a8.aTaps[tp] : 0.0f;
+      }
+    }
     for (int i = 0;; i += 2) {
       wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA);
+      if (AUD && i >= kAudioLag) wsAudioTile(a8, ring, c, t0, lead, i - kAudioLag, ptid, ht);
       if (i + 1 >= n) break;
       wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB);
+      if (AUD && i + 1 >= kAudioLag) wsAudioTile(a8, ring, c, t0, lead, i + 1 - kAudioLag, ptid, ht);
       if (i + 2 >= n) break;
     }
+    if constexpr (AUD)
+      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile(a8, ring, c, t0, lead, t, ptid, ht);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }
@@ -1374,7 +1474,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
   a.padShift = a8.padShift;
   a.planeStride = a8.planeStride;
   a.dbp = a8.dbp;
-  wsConsumers<KS, EPI, true>(a, smem, part, c, sh, t0, n, tid, a8.dbp != 0);
+  wsConsumers<KS, EPI, true, AUD>(a, smem, part, c, sh, t0, n, tid, a8.dbp != 0, ring, lead);
 }
 
 // ---- host side ------------------------------------------------------------------------------
@@ -1534,6 +1634,42 @@ hipError_t launchI8WsG(const I8DecArgs& a, int Wl, size_t lds, int grid, hipStre
   if (attrErr != hipSuccess) return attrErr;
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWsThreads), lds, stream, a, Wl);
   return hipGetLastError();
+}
+
+template <int KS, int G>
+hipError_t launchI8WsAudioG(const I8DecArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
+  auto kernel = &firI8WsKernel<KS, G, kEpiAm, true>;
+  const hipError_t attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kCfDynLdsMax);
+  if (attrErr != hipSuccess) return attrErr;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWsThreads), lds, stream, a, Wl);
+  return hipGetLastError();
+}
+
+template <int KS>
+hipError_t launchI8WsAudioKS(const I8DecArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
+  switch ((Wl + kWsPThreads - 1) / kWsPThreads) {
+    case 1: return launchI8WsAudioG<KS, 1>(a, Wl, lds, grid, stream);
+    case 2: return launchI8WsAudioG<KS, 2>(a, Wl, lds, grid, stream);
+    case 3: return launchI8WsAudioG<KS, 3>(a, Wl, lds, grid, stream);
+    default: return launchI8WsAudioG<KS, 4>(a, Wl, lds, grid, stream);
+  }
+}
+
+hipError_t launchI8WsAudioAny(const I8DecArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
+  switch (a.KS) {
+    case 1: return launchI8WsAudioKS<1>(a, Wl, lds, grid, stream);
+    case 2: return launchI8WsAudioKS<2>(a, Wl, lds, grid, stream);
+    case 3: return launchI8WsAudioKS<3>(a, Wl, lds, grid, stream);
+    case 4: return launchI8WsAudioKS<4>(a, Wl, lds, grid, stream);
+    case 5: return launchI8WsAudioKS<5>(a, Wl, lds, grid, stream);
+    case 6: return launchI8WsAudioKS<6>(a, Wl, lds, grid, stream);
+    case 7: return launchI8WsAudioKS<7>(a, Wl, lds, grid, stream);
+    case 8: return launchI8WsAudioKS<8>(a, Wl, lds, grid, stream);
+    case 9: return launchI8WsAudioKS<9>(a, Wl, lds, grid, stream);
+    case 10: return launchI8WsAudioKS<10>(a, Wl, lds, grid, stream);
+    default: return launchI8WsAudioKS<11>(a, Wl, lds, grid, stream);
+  }
 }
 
 template <int KS>
@@ -1825,6 +1961,60 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
     case 10: return launchI8DecKS<10>(a, lds, grid, epi, stream);
     default: return launchI8DecKS<11>(a, lds, grid, epi, stream);
   }
+}
+
+// int8 IQ -> FC FIR -> AM -> FF FIR in ONE launch of the wave-specialised kernel (firI8WsKernel<..,
+// true>): the consumers keep each tile's AM samples in an LDS ring, the producers run the audio FIR
+// from it. Returns hipErrorNotSupported when the shape or the policy does not take that kernel (the
+// caller then runs the two stages). amOut (nullable: AM not stored) = AM output 0; amHist[0, amH)
+// the AM samples before it.
+hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t tapCount, size_t decimation,
+                                   float* amOut, size_t nOut, const float* amHist, size_t amH, const float* aTaps,
+                                   size_t aT, size_t aD, float* aOut, size_t aN, hipStream_t stream) {
+  static_assert(kCfTileOut == 512, "the audio ring indexes AM samples by k >> 9");
+#ifdef GSDR_FORCE_POLICY
+  const uint32_t policy = GSDR_FORCE_POLICY;
+#else
+  const uint32_t policy = kernelPolicy();
+#endif
+  if ((policy & (GSDR_POLICY_NO_MFMA | GSDR_POLICY_NO_WS | GSDR_POLICY_PREFER_FFT)) != 0) return hipErrorNotSupported;
+  if (!firI8DecMfmaEligible(tapCount, decimation, iq) || aT == 0 || aT > (size_t)kAudioMaxTaps || aD == 0 ||
+      aD > 0x7fffffff || amH > 0x7fffffff || nOut == 0 || aN == 0)
+    return hipErrorNotSupported;
+  I8DecArgs a{};
+  a.sub = (int32_t)(reinterpret_cast<uintptr_t>(iq) & 3u);
+  a.iq4 = iq - a.sub;
+  a.taps = taps;
+  a.out = amOut;
+  a.D = (int32_t)(decimation < 1 ? 1 : decimation);
+  a.T = (int32_t)tapCount;
+  a.nOut = (int64_t)nOut;
+  a.nIn = (int64_t)(nOut - 1) * a.D + (int64_t)tapCount;
+  const int ksteps = (31 * a.D + a.T + 15) / 16;
+  a.KS = (ksteps + kCfWaves - 1) / kCfWaves;
+  const int64_t tiles = ((int64_t)nOut + kCfTileOut - 1) / kCfTileOut;
+  if (tiles > 0x7fffffff) return hipErrorNotSupported;
+  a.tiles = (int32_t)tiles;
+  a.Wu = 60 * a.D + 16 * a.KS;
+  const int Wl = std::min(a.Wu, (511 * a.D + a.T + 7) / 8);
+  if (Wl > 4 * kWsPThreads) return hipErrorNotSupported;
+  const CfLayout lay = cfPlaneLayout(a.D, a.KS, a.Wu, 4);
+  if (lay.planeStride == 0) return hipErrorNotSupported;
+  a.padShift = lay.padShift;
+  a.planeStride = lay.planeStride;
+  const size_t lds = 4 * (size_t)a.planeStride + 2 * kCfPartialBytes + sizeof(float) * kAmRing * kCfTileOut;
+  if (lds > (size_t)kCfDynLdsMax) return hipErrorNotSupported;
+  a.dbp = 1;
+  a.aTaps = aTaps;
+  a.aOut = aOut;
+  a.amHist = amHist;
+  a.aN = (int64_t)aN;
+  a.aT = (int32_t)aT;
+  a.aD = (int32_t)aD;
+  a.amH = (int32_t)amH;
+  const int grid = (int)(tiles < 256 ? tiles : 256);
+  if (hipError_t e = wsPrepare(stream, a.spinLimit, a.abortOut); e != hipSuccess) return e;
+  return launchI8WsAudioAny(a, Wl, lds, grid, stream);
 }
 
 }  // namespace gsdr_amd

@@ -46,6 +46,11 @@ hipError_t launchFirCfMfma(const float* x, const float* taps, size_t tapCount, s
 bool firI8DecMfmaEligible(size_t tapCount, size_t decimation, const void* in);
 hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCount, size_t decimation, void* out,
                               size_t nOut, int epi, hipStream_t stream);
+// The same RF stage with the AM -> FF audio FIR fused into the launch (gsdrInt8FirFCAmDemodFirFF);
+// hipErrorNotSupported when the wave-specialised kernel does not take the shape / policy.
+hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t tapCount, size_t decimation,
+                                   float* amOut, size_t nOut, const float* amHist, size_t amH, const float* aTaps,
+                                   size_t aT, size_t aD, float* aOut, size_t aN, hipStream_t stream);
 
 // cf32 (16-byte aligned) or int8 IQ (4-byte aligned) x real taps, long filters, D in {2,4,6,8,10}:
 // polyphase overlap-save FFT fast convolution (fir_fft.hip).

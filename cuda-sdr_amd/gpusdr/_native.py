@@ -49,6 +49,8 @@ def _declare(L):
         fn.restype = err
     L.gsdrInt8FirFCAmDemodCarry.argtypes = [sz, vp, sz, vp, vp, sz, vp, i32, vp]
     L.gsdrInt8FirFCAmDemodCarry.restype = err
+    L.gsdrInt8FirFCAmDemodFirFF.argtypes = [sz, vp, sz, vp, sz, vp, sz, i32, sz, vp, sz, vp, sz, i32, vp]
+    L.gsdrInt8FirFCAmDemodFirFF.restype = err
     for name in ("gsdrQuadAmDemod", "gsdrInt8ToNormFloat", "gsdrFloatToInt8"):
         fn = getattr(L, name)
         fn.argtypes = [vp, vp, sz, i32, vp]

@@ -159,6 +159,32 @@ def fir_am_i8_carry(taps: torch.Tensor, iq: torch.Tensor, decimation: int, num_o
     return out
 
 
+def am_chain_fused(taps: torch.Tensor, iq: torch.Tensor, decimation: int, rf_count: int,
+                   am_window: torch.Tensor, am_history: int, audio_taps: torch.Tensor, audio_decimation: int,
+                   audio_count: int, audio_out: torch.Tensor, store_am: bool = True) -> torch.Tensor:
+    """int8 IQ -> FIR -> AM -> audio FIR in one launch (gsdrInt8FirFCAmDemodFirFF): `rf_count` AM
+    samples land in am_window[am_history:] (unless store_am is False: then that part is scratch) and
+    `audio_count` audio samples of the FF FIR over am_window = [history | new AM] in `audio_out`."""
+    _require(taps, torch.float32, "taps")
+    _require(iq, torch.int8, "iq")
+    _require(am_window, torch.float32, "am_window")
+    _require(audio_taps, torch.float32, "audio_taps")
+    _require(audio_out, torch.float32, "audio_out")
+    d, da = max(1, int(decimation)), max(1, int(audio_decimation))
+    T, Ta = taps.numel(), audio_taps.numel()
+    if rf_count > 0 and (rf_count - 1) * d + T > iq.numel() // 2:
+        raise ValueError("input too short for the requested RF outputs")
+    if am_window.numel() < am_history + rf_count or audio_out.numel() < audio_count:
+        raise ValueError("am_window or audio_out too small")
+    if audio_count > 0 and (audio_count - 1) * da + Ta > am_history + rf_count:
+        raise ValueError("audio outputs need more AM samples than history + rf_count")
+    check(lib().gsdrInt8FirFCAmDemodFirFF(d, taps.data_ptr(), T, iq.data_ptr(), rf_count, am_window.data_ptr(),
+                                          am_history, 1 if store_am else 0, da, audio_taps.data_ptr(), Ta,
+                                          audio_out.data_ptr(), audio_count, _dev(iq), _stream(iq)),
+          "gsdrInt8FirFCAmDemodFirFF")
+    return audio_out
+
+
 def quad_am_demod(z: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _require(z, torch.complex64, "z")
     if out is None:

@@ -36,6 +36,26 @@ GSDR_API hipError_t gsdrFirCCAmDemod(size_t decimation, const hipFloatComplex* t
                                      hipStream_t stream);
 
 /*
+ * The C5 receive chain in ONE launch: int8 IQ -> FC FIR (taps, decimation) -> AM -> FF audio FIR
+ * (audioTaps, audioDecimation). amWindow = [amHistory AM samples carried from before | rfCount new];
+ * the call computes
+ *     gsdrInt8FirFCAmDemod(decimation, taps, tapCount, inputIq, amWindow + amHistory, rfCount)
+ *     gsdrFirFF(audioDecimation, audioTaps, audioTapCount, amWindow, audioOut, audioCount)
+ * with (audioCount - 1) audioDecimation + audioTapCount <= amHistory + rfCount. On the
+ * wave-specialised int8 matrix-core kernel (the C5 RF shape) the AM samples stay on chip: each
+ * tile's AM goes to an LDS ring and the kernel's producer waves run the audio FIR from it (<= 256
+ * audio taps; each audio output a 64-lane sum of 4-tap partials - the same terms as gsdrFirFF in
+ * another order). storeAm = 0 leaves amWindow[amHistory..] unspecified (not written by the fused
+ * kernel; other shapes use it as the intermediate); 1 stores the AM samples there as the first call
+ * would. Other shapes and policies run the two calls.
+ */
+GSDR_API hipError_t gsdrInt8FirFCAmDemodFirFF(size_t decimation, const float* taps, size_t tapCount,
+                                              const int8_t* inputIq, size_t rfCount, float* amWindow,
+                                              size_t amHistory, int storeAm, size_t audioDecimation,
+                                              const float* audioTaps, size_t audioTapCount, float* audioOut,
+                                              size_t audioCount, int32_t device, hipStream_t stream);
+
+/*
  * Streaming form of gsdrInt8FirFCAmDemod: the same outputs, and the history the next call needs
  * (input samples [outputCount * decimation, (outputCount - 1) * decimation + tapCount), i.e. the
  * last tapCount - decimation samples) is copied to carryIq in the same launch. carryIq may alias

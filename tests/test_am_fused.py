@@ -1,0 +1,126 @@
+"""The C5 receive chain in ONE launch (gsdrInt8FirFCAmDemodFirFF: int8 IQ -> FC FIR -> AM -> FF audio
+FIR, the AM samples in an LDS ring of the wave-specialised int8 MFMA kernel, the audio FIR on its
+producer waves) against the float64 oracle chain, and against the two reference calls it stands for
+(gsdrInt8FirFCAmDemod then gsdrFirFF over [AM history | new AM], QuadAmDemod.cpp:93-98 + Fir.cpp:229-269):
+the AM samples bit for bit, the audio within the oracle bound (the audio sum runs in another order)."""
+import numpy as np
+import pytest
+
+FIR_TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def ops():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from gpusdr import ops
+    return ops
+
+
+def _expected_audio(orc, am64, rf_bound, audio_taps, Da, n):
+    """float64 audio FIR over the float64 AM stream + the bound: the RF FIR bound and the sqrt
+    rounding carried through |audio taps|, plus the audio FIR's own bound."""
+    audio, audio_bound = orc.fir_f64(audio_taps, am64.astype(np.float32), Da, n)
+    carried, _ = orc.fir_f64(np.abs(audio_taps), (FIR_TOL * (rf_bound + am64)).astype(np.float32), Da, n)
+    return audio, carried + FIR_TOL * audio_bound + 1e-30
+
+
+def _run(ops, orc, T, D, Ta, Da, n_hist_rf, n_rf, H, seed, store=True, check_kernel=True):
+    """RF outputs [0, n_hist_rf) by the plain call (the history), then the fused call over RF outputs
+    [n_hist_rf, n_hist_rf + n_rf) with the last H of the earlier AM samples as its history."""
+    import torch
+    rng = np.random.default_rng(seed)
+    rf = orc.lowpass_taps(T, 0.4 / D, "blackman")
+    au = orc.lowpass_taps(Ta, 0.4 / Da)
+    n_all = n_hist_rf + n_rf
+    iq = rng.integers(-128, 128, size=2 * ((n_all - 1) * D + T)).astype(np.int8)
+    dev = torch.from_numpy(iq).cuda()
+    rf_d, au_d = torch.from_numpy(rf).cuda(), torch.from_numpy(au).cuda()
+    if check_kernel:
+        assert ops.fir_kernel_class(dev, rf_d, D, int8_iq=True) == "i8-dec-mfma"
+    am_all = torch.zeros(n_all, dtype=torch.float32, device="cuda")
+    if n_hist_rf:
+        ops.fir(rf_d, dev, D, n_hist_rf, out=am_all[:n_hist_rf], am=True, int8_iq=True)
+    window = am_all[n_hist_rf - H:]
+    n_audio = (H + n_rf - Ta) // Da + 1
+    audio = torch.full((n_audio,), float("nan"), dtype=torch.float32, device="cuda")
+    ops.am_chain_fused(rf_d, dev[2 * n_hist_rf * D:], D, n_rf, window, H, au_d, Da, n_audio, audio, store_am=store)
+    # the two reference calls over the same input
+    am_ref = torch.empty(n_rf, dtype=torch.float32, device="cuda")
+    ops.fir(rf_d, dev[2 * n_hist_rf * D:], D, n_rf, out=am_ref, am=True, int8_iq=True)
+    win_ref = torch.cat([am_all[n_hist_rf - H: n_hist_rf], am_ref])
+    audio_ref = ops.fir(au_d, win_ref, Da, n_audio)
+    torch.cuda.synchronize()
+    x = orc.int8_to_float(iq).view(np.complex64)
+    y, rf_bound = orc.fir_f64(rf, x, D, n_all)
+    am64 = np.abs(y)
+    lo = n_hist_rf - H
+    want, bound = _expected_audio(orc, am64[lo:], rf_bound[lo:], au, Da, n_audio)
+    got = audio.cpu().numpy()
+    ref = audio_ref.cpu().numpy()
+    assert np.all(np.isfinite(got))
+    assert np.all(np.abs(got - want) <= bound), np.max(np.abs(got - want) / bound)
+    assert np.all(np.abs(ref - want) <= bound)
+    assert np.all(np.abs(got - ref) <= 2 * bound)
+    if store:  # the AM samples are the plain call's, bit for bit
+        assert am_all[n_hist_rf:].cpu().numpy().tobytes() == am_ref.cpu().numpy().tobytes()
+    return got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,D,Ta,Da,n_rf", [
+    (1023, 10, 255, 20, 200_000),   # C5's filters, ~390 tiles: every block has a lead tile
+    (1023, 10, 255, 20, 1_000),     # 2 tiles: blocks of one tile (lead + one)
+    (1023, 10, 255, 20, 255),       # one tile, exactly one audio output
+    (255, 5, 63, 8, 70_001),        # ragged last tile
+    (511, 8, 256, 3, 40_000),       # 256 audio taps (the most the ring stage takes), D_a = 3
+    (160, 16, 17, 64, 30_000),      # D_a > a tile's share of outputs per wave batch
+    (64, 2, 9, 1, 9_000),           # D_a = 1: 57 outputs per tile per wave
+])
+def test_fused_chain_matches_oracle(ops, orc, T, D, Ta, Da, n_rf):
+    _run(ops, orc, T, D, Ta, Da, 0, n_rf, 0, seed=T + n_rf)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H", [1, 254, 3000])
+def test_fused_chain_with_am_history(ops, orc, H):
+    """History in front of the new AM samples (the chunked / resident executors' carried ra samples);
+    H > Ta: the first audio windows lie wholly in the history."""
+    _run(ops, orc, 1023, 10, 255, 20, 5000, 60_000, H, seed=H)
+
+
+@pytest.mark.gpu
+def test_fused_chain_without_am_store(ops, orc):
+    """store_am = False (the sharded C5 step: nothing downstream reads the AM samples): same audio."""
+    a = _run(ops, orc, 1023, 10, 255, 20, 0, 100_000, 0, seed=3, store=False)
+    b = _run(ops, orc, 1023, 10, 255, 20, 0, 100_000, 0, seed=3, store=True)
+    assert a.tobytes() == b.tobytes()
+
+
+@pytest.mark.gpu
+def test_fused_chain_fallback_shapes(ops, orc):
+    """Shapes / policies the fused kernel does not take run the two calls: > 256 audio taps; the
+    barrier-synchronous policy."""
+    _run(ops, orc, 255, 5, 300, 4, 0, 20_000, 0, seed=7)
+    prev = ops.set_kernel_policy(ops.POLICY_NO_WS)
+    try:
+        _run(ops, orc, 1023, 10, 255, 20, 0, 20_000, 0, seed=8, check_kernel=False)
+    finally:
+        ops.set_kernel_policy(prev)
+
+
+@pytest.mark.gpu
+def test_fused_chain_rejects_short_am(ops, orc):
+    import torch
+    rf = torch.from_numpy(orc.lowpass_taps(1023, 0.04)).cuda()
+    au = torch.from_numpy(orc.lowpass_taps(255, 0.02)).cuda()
+    iq = torch.zeros(2 * (999 * 10 + 1023), dtype=torch.int8, device="cuda")
+    win = torch.empty(1000, dtype=torch.float32, device="cuda")
+    out = torch.empty(100, dtype=torch.float32, device="cuda")
+    with pytest.raises(ValueError):
+        ops.am_chain_fused(rf, iq, 10, 1000, win, 0, au, 20, 100, out)
+    from gpusdr._native import lib
+    r = lib().gsdrInt8FirFCAmDemodFirFF(10, rf.data_ptr(), 1023, iq.data_ptr(), 1000, win.data_ptr(), 0, 1, 20,
+                                        au.data_ptr(), 255, out.data_ptr(), 100, 0, None)
+    assert r != 0
