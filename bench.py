@@ -286,7 +286,8 @@ class AmChainSharded:
         audio FIR's direct-form flops."""
         g = self.geom
         kind, fl, peak = kernel_compute(self.kernel_class, g.rf_outputs, self.T, self.D)
-        return 2 * (g.halo + self.L) + 4 * g.outputs, (f"RF: {kind}; audio FIR: fp32 VALU direct form",
+        return 2 * (g.halo + self.L) + 4 * g.outputs, (f"RF: {kind}; audio FIR: fp32 VALU on the RF kernel's "
+                                                       "producer waves (N = 1) / direct form",
                                                        fl + g.outputs * self.Ta * 2, peak)
 
 
@@ -458,10 +459,13 @@ def kernel_name(chain):
     if isinstance(chain, AmChainSharded):
         body = {"fft": "firFftKernel", "i8-dec-mfma": "firI8WsKernel", "valu": "firLdsKernel"}.get(
             chain.kernel_class, chain.kernel_class)
-        return (f"whole C5 step: gsdrInt8FirFCAmDemod ({body}) bulk + head, gsdrFirFF audio "
-                "(firDecFFKernel); HIP events around the step")
+        if chain.single:
+            return (f"whole C5 step: gsdrInt8FirFCAmDemodFirFF ({body}<.., AUD>: RF FIR + AM + audio FIR in one "
+                    "launch); HIP events around the step")
+        return (f"whole C5 step: gsdrInt8FirFCAmDemodFirFF bulk ({body}<.., AUD>), then the head: "
+                "gsdrInt8FirFCAmDemod + gsdrFirFF over the head's audio windows; HIP events around the step")
     if isinstance(chain, AmChainRunner):
-        return (f"gsdrAmChain {chain.mode} step graph (RF FIR+AM, audio FIR, history copies; "
+        return (f"gsdrAmChain {chain.mode} step graph (RF FIR+AM+audio FIR fused per launch, history copies; "
                 "HIP events around the whole step)")
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"

@@ -641,7 +641,7 @@ constexpr int kWsSpinLimit = 1 << 22;                       // default s_sleep(1
 // the audio outputs of tile i - kAudioLag after producing the planes of tile i.
 constexpr int kAmRing = 8;
 constexpr int kAudioLag = 3;
-constexpr int kAudioMaxTaps = 256;  // 4 taps per lane
+constexpr int kAudioMaxTaps = 256;  // 8 tap groups of 32 per output slot
 
 struct WsCtl {
   int planesFull[2];
@@ -1328,13 +1328,20 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 // Fused audio stage, producer side: the audio outputs of block-local tile t (global tile t0 + t) -
 // those whose window ends in that tile's AM range (tile 0 of the launch: also windows ending
 // before AM sample 0, in the history) - from the AM ring the consumers fill (tiles t - 1 and t are
-// in it: a window spans at most 256 AM samples), then amFree. Wave pw takes outputs jLo + pw + 4 b;
-// lane l accumulates taps l + 64 m (m < 4, conflict-free ring reads), then a wave sum per output.
+// in it: a window spans at most 256 AM samples), then amFree. A wave takes 8 outputs at a time,
+// jb + 4 o (o < 8, wave pw from jb = jLo + pw): lane l works on slot o = l / 8 with the taps
+// q + 8 u of its tap group q = l % 8 (u < 32; 32 LDS reads and FMAs, the 8 lanes of a slot reading
+// consecutive AM samples), then the slot's 8 partial sums meet in 3 DPP adds - no LDS round trip
+// (a 64-lane sum per output through ds_bpermute serialised ~50 LDS round trips per tile and made the
+// producers, who feed the matrix cores, the bottleneck: C5 0.18 -> 0.71 ms per step).
 // The lead tile (the previous block's last, computed for the ring only) has no outputs here.
+constexpr int kAudioTapsPerLane = kAudioMaxTaps / 8;
+
 __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* ring, WsCtl* c, int t0, bool lead, int t,
-                                            int ptid, const float (&ht)[4]) {
+                                            int ptid, const float (&ht)[kAudioTapsPerLane]) {
   const int lane = ptid & (kWave - 1);
   const int pw = ptid >> 6;
+  const int o = lane >> 3, q = lane & 7;
   if (!(lead && t == 0)) {
     wsWait(c, &c->amFull, kCfWaves * (t + 1));
     const int64_t g = (int64_t)(t0 + t);
@@ -1347,34 +1354,36 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
     int64_t jHi = firstJ((g + 1) * kCfTileOut);
     if (jHi > a.aN) jHi = a.aN;
     for (int64_t jb = jLo + pw; jb < jHi; jb += 8 * kWsProducers) {
-      float s[8];
+      const int64_t j = jb + kWsProducers * o;
+      const int64_t k0 = j * a.aD - a.amH;  // this slot's window: AM samples k0 .. k0 + aT - 1
+      float s = 0.0f;
+      if (jb * a.aD - a.amH >= 0) {  // wave-uniform: every window of the batch lies in the ring
+        const int kk0 = (int)(k0 - (int64_t)kCfTileOut * t0) + q;  // block-local AM index
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        s[b] = 0.0f;
-        const int64_t j = jb + kWsProducers * b;
-        if (j < jHi) {  // wave-uniform
-          const int64_t k0 = j * a.aD - a.amH;  // the window's first AM sample
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const int tp = lane + kWave * m;
-            const int64_t k = k0 + tp;
-            if (tp < a.aT) {
-              const float x = k >= 0 ? ring[(((int)(k >> 9) - t0) & (kAmRing - 1)) * kCfTileOut + (int)(k & 511)]
-                                     : a.amHist[a.amH + k];
-              s[b] = fmaf(ht[m], x, s[b]);
-            }
-          }
+        for (int u = 0; u < kAudioTapsPerLane; ++u)
+          s = fmaf(ht[u], ring[(kk0 + 8 * u) & (kAmRing * kCfTileOut - 1)], s);
+      } else {  // windows reaching into the history (the launch's first outputs)
+        // buffer loads (range-checked): a pointer select between the ring and the history would
+        // compile to FLAT loads
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.amHist), (short)0, 4 * a.amH,
+                                                          0x00020000);
+#pragma unroll 4
+        for (int u = 0; u < kAudioTapsPerLane; ++u) {
+          const int64_t k = k0 + q + 8 * u;
+          float x;
+          if (k >= 0)
+            x = ring[(int)(k - (int64_t)kCfTileOut * t0) & (kAmRing * kCfTileOut - 1)];
+          else
+            x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * (a.amH + k)), 0, 0));
+          s = fmaf(ht[u], x, s);
         }
       }
-#pragma unroll
-      for (int b = 0; b < 8; ++b) s[b] = waveSum(s[b]);
-      if (lane == 0) {
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          const int64_t j = jb + kWsProducers * b;
-          if (j < jHi) a.aOut[j] = s[b];
-        }
-      }
+      // the slot's 8 tap groups: half-mirror, then the two quad swaps (every lane of the 8 ends
+      // with the sum)
+      s += dppF<0x141>(s);
+      s += dppF<0x4E>(s);
+      s += dppF<0xB1>(s);
+      if (q == 0 && j < jHi) a.aOut[j] = s;
     }
   }
   wsSignal(&c->amFree, lane);
@@ -1440,13 +1449,11 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
     const i4v r1 = wsI8TileRsrc(a8, t0 + 1, n > 1);
 #pragma unroll
     for (int j = 0; j < G; ++j) wsI8LoadGroup<G>(r1, Wl, ptid, j, wB);
-    float ht[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // audio taps lane + 64 m
-    if constexpr (AUD) {
+    float ht[kAudioTapsPerLane];  // audio taps (lane % 8) + 8 u
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int tp = lane + kWave * m;
-        ht[m] = tp < a8.aT ? a8.aTaps[tp] : 0.0f;
-      }
+    for (int u = 0; u < kAudioTapsPerLane; ++u) {
+      const int tp = (lane & 7) + 8 * u;
+      ht[u] = AUD && tp < a8.aT ? a8.aTaps[tp] : 0.0f;
     }
     for (int i = 0;; i += 2) {
       wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA);

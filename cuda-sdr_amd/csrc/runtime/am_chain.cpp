@@ -12,9 +12,9 @@
 //
 //   staging[p] = [ r history | L new ]  int8 IQ     (p = step parity; the carry goes to 1 - p)
 //   am         = [ ra history | L/D new ] f32
-//   graph(p):  gsdrInt8FirFCAmDemod(staging[p] -> am + ra)        (L/D outputs)
+//   graph(p):  gsdrInt8FirFCAmDemodFirFF(staging[p] -> am + ra,   (L/D RF outputs and, in the same
+//                                        am -> audio)             launch, L/(D Da) audio outputs)
 //              copy staging[p][L, L + r) -> staging[1-p][0, r)     (RF history)
-//              gsdrFirFF(am -> audio)                              (L/(D Da) outputs)
 //              copy am[La, La + ra) -> am[0, ra)                   (audio history)
 //
 // The first step has its own graph (input at staging[0] + r, AM written to the end of the window).
@@ -149,9 +149,10 @@ struct gsdrAmChainImpl {
     const size_t amStart = firstStep ? ra + La - n1 : 0;  // first step: AM at the end of the window
     const int8_t* in = firstStep ? staging[p] + 2 * r : staging[p];
     const size_t nRf = firstStep ? n1 : La;
-    AMC_TRY(gsdrInt8FirFCAmDemod(D, taps, T, in, am + (firstStep ? amStart : ra), nRf, device, stream));
+    // RF FIR + AM + audio FIR in one launch (the AM samples kept: the next step's audio history)
+    AMC_TRY(gsdrInt8FirFCAmDemodFirFF(D, taps, T, in, nRf, am + amStart, firstStep ? 0 : ra, 1, Da, audioTaps, Ta,
+                                      audio, firstStep ? na1 : naSteady, device, stream));
     AMC_TRY(hipMemcpyAsync(staging[1 - p], staging[p] + 2 * L, 2 * r, hipMemcpyDeviceToDevice, stream));
-    AMC_TRY(gsdrFirFF(Da, audioTaps, Ta, am + amStart, audio, firstStep ? na1 : naSteady, device, stream));
     AMC_TRY(hipMemcpyAsync(am, am + La, sizeof(float) * ra, hipMemcpyDeviceToDevice, stream));
     return hipSuccess;
   }
@@ -170,8 +171,8 @@ struct gsdrAmChainImpl {
     const size_t end = ra + nChunks * La;  // the AM window ends here in both cases
     const size_t amStart = steps == 0 ? end - nRf : 0;
     const int8_t* rfIn = steps == 0 ? in : in - 2 * r;
-    AMC_TRY(gsdrInt8FirFCAmDemod(D, taps, T, rfIn, amBig + (end - nRf), nRf, device, stream));
-    AMC_TRY(gsdrFirFF(Da, audioTaps, Ta, amBig + amStart, out, residentAudio(nChunks), device, stream));
+    AMC_TRY(gsdrInt8FirFCAmDemodFirFF(D, taps, T, rfIn, nRf, amBig + amStart, end - nRf - amStart, 1, Da, audioTaps,
+                                      Ta, out, residentAudio(nChunks), device, stream));
     AMC_TRY(hipMemcpyAsync(amBig, amBig + end - ra, sizeof(float) * ra, hipMemcpyDeviceToDevice, stream));
     return hipSuccess;
   }
@@ -194,12 +195,12 @@ struct gsdrAmChainImpl {
       const size_t nRf = f ? n1 : La;
       const int8_t* rfIn = f ? in : (i == 0 ? staging[p0] : in + 2 * (L * i - r));
       const size_t amEnd = ra + (i + 1) * La;  // chunk i's AM ends here (first step: n1 < La of it)
-      AMC_TRY(gsdrInt8FirFCAmDemod(D, taps, T, rfIn, amMulti + amEnd - nRf, nRf, device, stream));
-      // one stream: forking chunk i's audio FIR onto a second captured stream beside chunk i+1's
-      // RF launch measured 3.5x slower per chunk (cross-stream graph dependencies)
+      // one launch per chunk: RF FIR + AM + the chunk's audio outputs (gsdrInt8FirFCAmDemodFirFF; r02
+      // forked each chunk's audio FIR onto a second captured stream: 3.5x slower per chunk)
       const size_t na = f ? na1 : naSteady;
-      AMC_TRY(gsdrFirFF(Da, audioTaps, Ta, amMulti + (f ? amEnd - n1 : amEnd - La - ra), out + pos, na, device,
-                        stream));
+      const size_t amWin = f ? amEnd - n1 : amEnd - La - ra;
+      AMC_TRY(gsdrInt8FirFCAmDemodFirFF(D, taps, T, rfIn, nRf, amMulti + amWin, amEnd - nRf - amWin, 1, Da, audioTaps,
+                                        Ta, out + pos, na, device, stream));
       pos += na;
     }
     const int pn = (int)((startStep + nChunks) & 1);

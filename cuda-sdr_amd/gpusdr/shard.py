@@ -219,10 +219,11 @@ class HaloRing:
 
 class AmChainShard:
     """One rank's state for the time-sharded AM receive chain (ChainShardGeometry) on the GPU:
-    buffer [halo | segment] of int8 IQ, the RF FIR + AM (gsdrInt8FirFCAmDemod) split into the bulk
-    (segment-only windows, launched while the halo exchange is in flight) and the head (windows
-    reaching into the halo), then the audio FIR (gsdrFirFF) over the step's AM samples.
-    Weak scaling: every rank processes seg_len samples per step."""
+    buffer [halo | segment] of int8 IQ. One rank: the whole chain - RF FIR + AM + audio FIR - is ONE
+    launch (gsdrInt8FirFCAmDemodFirFF, the AM samples never leave the chip). Several ranks: the bulk
+    launch (segment-only RF windows and the audio outputs over them, fused; it runs while the halo
+    exchange is in flight) and the head (RF windows reaching into the halo, then the first audio
+    outputs, which read those AM samples). Weak scaling: every rank processes seg_len samples per step."""
 
     def __init__(self, geom: ChainShardGeometry, rf_taps, audio_taps, device, stage: bool = False, buf=None):
         """`buf`: an int8 view of 2 (halo + seg_len) bytes to work in (default: a fresh buffer). Views
@@ -243,16 +244,31 @@ class AmChainShard:
         self.am = torch.empty(geom.rf_outputs, dtype=torch.float32, device=device)
         self.out = torch.empty(geom.outputs, dtype=torch.float32, device=device)
 
+    @property
+    def head_audio(self) -> int:
+        """Audio outputs whose window reaches into the head's AM samples [0, head_rf): j Da < head_rf
+        (head_rf = halo / D is a multiple of Da by the halo's rounding)."""
+        g = self.geom
+        return min(g.outputs, -(-g.head_rf // g.audio_decimation))
+
     def _bulk(self):
+        """RF outputs [head_rf, rf_outputs) and, in the same launch, the audio outputs whose windows
+        lie in them (gsdrInt8FirFCAmDemodFirFF); the AM samples are kept for the head's audio."""
         from . import ops
         g = self.geom
-        ops.fir(self.rf_taps, self.seg, g.decimation, g.rf_outputs - g.head_rf, out=self.am[g.head_rf:],
-                am=True, int8_iq=True)
+        n_bulk = g.rf_outputs - g.head_rf
+        ha = self.head_audio
+        ops.am_chain_fused(self.rf_taps, self.seg, g.decimation, n_bulk, self.am[g.head_rf:], 0, self.audio_taps,
+                           g.audio_decimation, g.outputs - ha, self.out[ha:], store_am=True)
 
     def _head(self):
+        """RF outputs [0, head_rf) (they read the halo), then the audio outputs that read them."""
         from . import ops
         g = self.geom
         ops.fir(self.rf_taps, self.buf, g.decimation, g.head_rf, out=self.am[: g.head_rf], am=True, int8_iq=True)
+        ha = self.head_audio
+        if ha > 0:
+            ops.fir(self.audio_taps, self.am, g.audio_decimation, ha, out=self.out[:ha])
 
     def step(self, carry_to=None, carry: bool = True):
         """One step over the segment currently in self.seg; the audio lands in self.out. A single
@@ -263,10 +279,11 @@ class AmChainShard:
         from . import ops
         g = self.geom
         if g.world == 1:
-            ops.fir(self.rf_taps, self.buf, g.decimation, g.rf_outputs, out=self.am, am=True, int8_iq=True)
+            # ONE launch: RF FIR + AM + the audio FIR (the AM samples stay on chip, not stored)
+            ops.am_chain_fused(self.rf_taps, self.buf, g.decimation, g.rf_outputs, self.am, 0, self.audio_taps,
+                               g.audio_decimation, g.outputs, self.out, store_am=False)
             if carry:
                 (self.ring.halo if carry_to is None else carry_to).copy_(self.ring.tail)
         else:
             self.ring.step(self._bulk, self._head)
-        ops.fir(self.audio_taps, self.am, g.audio_decimation, g.outputs, out=self.out)
         return self.out
