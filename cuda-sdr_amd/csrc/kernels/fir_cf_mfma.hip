@@ -1298,12 +1298,20 @@ __device__ __forceinline__ void wsI8WaitWindow(I8WsWindow<G>& w) {
 }
 
 // Producer, tile i: wCur holds tile i's window (complete after the wait), wNext tile i + 1's.
-template <int G>
+// `pre` runs once the window has landed and before this tile's loads of tile i + 2 are issued (the
+// fused audio stage: its output stores then sit in front of those loads in the vmcnt order, so the
+// next window wait does not also wait for loads issued this iteration).
+struct NoPre {
+  __device__ void operator()() const {}
+};
+
+template <int G, typename Pre = NoPre>
 __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
-                                                 int i, int ptid, I8WsWindow<G>& wCur) {
+                                                 int i, int ptid, I8WsWindow<G>& wCur, const Pre& pre = Pre{}) {
   const int lane = ptid & (kWave - 1);
   const int set = i & 1;
   wsI8WaitWindow<2 * G>(wCur);
+  pre();
   wsWait(c, &c->planesFree[set], kCfWaves * (i >> 1));
   int8_t* planes = smem + set * 2 * a.planeStride;
   const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
@@ -1456,11 +1464,13 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
       ht[u] = AUD && tp < a8.aT ? a8.aTaps[tp] : 0.0f;
     }
     for (int i = 0;; i += 2) {
-      wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA);
-      if (AUD && i >= kAudioLag) wsAudioTile(a8, ring, c, t0, lead, i - kAudioLag, ptid, ht);
+      wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
+        if (AUD && i >= kAudioLag) wsAudioTile(a8, ring, c, t0, lead, i - kAudioLag, ptid, ht);
+      });
       if (i + 1 >= n) break;
-      wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB);
-      if (AUD && i + 1 >= kAudioLag) wsAudioTile(a8, ring, c, t0, lead, i + 1 - kAudioLag, ptid, ht);
+      wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
+        if (AUD && i + 1 >= kAudioLag) wsAudioTile(a8, ring, c, t0, lead, i + 1 - kAudioLag, ptid, ht);
+      });
       if (i + 2 >= n) break;
     }
     if constexpr (AUD)
@@ -2005,7 +2015,21 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
   a.Wu = 60 * a.D + 16 * a.KS;
   const int Wl = std::min(a.Wu, (511 * a.D + a.T + 7) / 8);
   if (Wl > 4 * kWsPThreads) return hipErrorNotSupported;
-  const CfLayout lay = cfPlaneLayout(a.D, a.KS, a.Wu, 4);
+  // the layout search costs ~1 ms of host time: cached per (D, KS) like the other launchers' (an
+  // uncached search per call starved the GPU between eager launches: 0.70 ms per C5 step)
+  static std::mutex layMu;
+  static int layD = -1, layKS = -1;
+  static CfLayout layCached{};
+  CfLayout lay;
+  {
+    std::lock_guard<std::mutex> lock(layMu);
+    if (layD != a.D || layKS != a.KS) {
+      layCached = cfPlaneLayout(a.D, a.KS, a.Wu, 4);
+      layD = a.D;
+      layKS = a.KS;
+    }
+    lay = layCached;
+  }
   if (lay.planeStride == 0) return hipErrorNotSupported;
   a.padShift = lay.padShift;
   a.planeStride = lay.planeStride;
