@@ -640,7 +640,8 @@ constexpr int kWsSpinLimit = 1 << 22;                       // default s_sleep(1
 // Fused audio stage (firI8WsKernel<.., AUD>): AM ring of kAmRing tiles in LDS; the producers compute
 // the audio outputs of tile i - kAudioLag after producing the planes of tile i.
 constexpr int kAmRing = 8;
-constexpr int kAudioLag = 3;
+constexpr int kAudioLag = 5;
+constexpr int kAmRingMirror = 256;  // ring[4096 + i] = ring[i] for i < 256: no wrap inside a window
 constexpr int kAudioMaxTaps = 256;  // 8 tap groups of 32 per output slot
 
 struct WsCtl {
@@ -864,7 +865,10 @@ __device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* pa
       const float v = __builtin_amdgcn_sqrtf(fmaf(yi, yi, yq * yq)) * ldexpf(1.0f / 127.0f, -sh);
       // slot j mod kAmRing is free once the producers finished the audio outputs of tile j - kAmRing + 1
       if (j - kAmRing + 2 > 0) wsWait(c, &c->amFree, kWsProducers * (j - kAmRing + 2));
-      ring[(j & (kAmRing - 1)) * kCfTileOut + 32 * orow + (lane & 31)] = k < a.nOut ? v : 0.0f;
+      const int pos = (j & (kAmRing - 1)) * kCfTileOut + 32 * orow + (lane & 31);
+      const float rv = k < a.nOut ? v : 0.0f;
+      ring[pos] = rv;
+      if (pos < kAmRingMirror) ring[kAmRing * kCfTileOut + pos] = rv;
       wsSignal(&c->amFull, lane);
       // the lead tile belongs to the previous block (computed here only for the audio windows)
       if (a.out != nullptr && k < a.nOut && !(lead && j == 0)) reinterpret_cast<float*>(a.out)[k] = v;
@@ -1298,9 +1302,9 @@ __device__ __forceinline__ void wsI8WaitWindow(I8WsWindow<G>& w) {
 }
 
 // Producer, tile i: wCur holds tile i's window (complete after the wait), wNext tile i + 1's.
-// `pre` runs once the window has landed and before this tile's loads of tile i + 2 are issued (the
-// fused audio stage: its output stores then sit in front of those loads in the vmcnt order, so the
-// next window wait does not also wait for loads issued this iteration).
+// `pre` runs while the window is still landing (the fused audio stage hides its work under that
+// wait; its few output stores sit behind tile i + 1's loads in the vmcnt order - issued a tile
+// earlier - and in front of tile i + 2's, so no window wait waits for loads issued this iteration).
 struct NoPre {
   __device__ void operator()() const {}
 };
@@ -1310,8 +1314,8 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
                                                  int i, int ptid, I8WsWindow<G>& wCur, const Pre& pre = Pre{}) {
   const int lane = ptid & (kWave - 1);
   const int set = i & 1;
-  wsI8WaitWindow<2 * G>(wCur);
   pre();
+  wsI8WaitWindow<2 * G>(wCur);
   wsWait(c, &c->planesFree[set], kCfWaves * (i >> 1));
   int8_t* planes = smem + set * 2 * a.planeStride;
   const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
@@ -1366,10 +1370,11 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
       const int64_t k0 = j * a.aD - a.amH;  // this slot's window: AM samples k0 .. k0 + aT - 1
       float s = 0.0f;
       if (jb * a.aD - a.amH >= 0) {  // wave-uniform: every window of the batch lies in the ring
-        const int kk0 = (int)(k0 - (int64_t)kCfTileOut * t0) + q;  // block-local AM index
+        // block-local AM index, wrapped once: the mirror behind the ring keeps the window contiguous
+        // (immediate-offset LDS reads)
+        const float* w = ring + (((int)(k0 - (int64_t)kCfTileOut * t0) + q) & (kAmRing * kCfTileOut - 1));
 #pragma unroll
-        for (int u = 0; u < kAudioTapsPerLane; ++u)
-          s = fmaf(ht[u], ring[(kk0 + 8 * u) & (kAmRing * kCfTileOut - 1)], s);
+        for (int u = 0; u < kAudioTapsPerLane; ++u) s = fmaf(ht[u], w[8 * u], s);
       } else {  // windows reaching into the history (the launch's first outputs)
         // buffer loads (range-checked): a pointer select between the ring and the history would
         // compile to FLAT loads
@@ -2033,7 +2038,7 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
   if (lay.planeStride == 0) return hipErrorNotSupported;
   a.padShift = lay.padShift;
   a.planeStride = lay.planeStride;
-  const size_t lds = 4 * (size_t)a.planeStride + 2 * kCfPartialBytes + sizeof(float) * kAmRing * kCfTileOut;
+  const size_t lds = 4 * (size_t)a.planeStride + 2 * kCfPartialBytes + sizeof(float) * (kAmRing * kCfTileOut + kAmRingMirror);
   if (lds > (size_t)kCfDynLdsMax) return hipErrorNotSupported;
   a.dbp = 1;
   a.aTaps = aTaps;
