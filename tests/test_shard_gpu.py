@@ -128,7 +128,7 @@ def test_c4_shape_time_sharded_on_hip(tmp_path, orc, world):
     assert np.all(err <= FIR_TOL * bound + 1e-30), float(np.max(err / (bound + 1e-30)))
 
 
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [1, 2, 8])  # 1: the single-rank step is ONE fused launch
 def test_c5_chain_time_sharded_cascaded_halo(tmp_path, orc, world):
     from gpusdr.shard import ChainShardGeometry
     T, D, Ta, Da, L = 1023, 10, 255, 20, 40_000
