@@ -2001,7 +2001,7 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
 #endif
   if ((policy & (GSDR_POLICY_NO_MFMA | GSDR_POLICY_NO_WS | GSDR_POLICY_PREFER_FFT)) != 0) return hipErrorNotSupported;
   if (!firI8DecMfmaEligible(tapCount, decimation, iq) || aT == 0 || aT > (size_t)kAudioMaxTaps || aD == 0 ||
-      aD > 0x7fffffff || amH > 0x7fffffff || nOut == 0 || aN == 0)
+      aD > 0x7fffffff || amH > 0x1fffffff || nOut == 0 || aN == 0)  // history: one 32-bit buffer range
     return hipErrorNotSupported;
   I8DecArgs a{};
   a.sub = (int32_t)(reinterpret_cast<uintptr_t>(iq) & 3u);
