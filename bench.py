@@ -760,7 +760,9 @@ def main():
             cpu = cpu_baseline(args.workload)
         traffic = load_traffic(args.workload)
         rf_traffic = None
-        if args.workload == "c5":  # the PMC summary is of the RF bulk kernel, the timed region the whole step
+        if args.workload == "c5" and not (world == 1 and args.c5_mode == "sharded"):
+            # the PMC summary is of the fused N = 1 step's one launch; elsewhere the timed region
+            # holds more launches (bulk + head, or an executor graph)
             rf_traffic, traffic = traffic, None
         line = {
             "metric": METRIC,
@@ -800,7 +802,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
-                **({"traffic_rf_bulk_kernel": rf_traffic} if rf_traffic is not None else {}),
+                **({"traffic_fused_rf_audio_kernel": rf_traffic} if rf_traffic is not None else {}),
                 "avg_launch_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": bytes_,
                 "compute": {"kind": compute_kind, "achieved_tflops": achieved_t, "peak_tflops": peak_t,
