@@ -640,20 +640,27 @@ def node_path(ops, device, kernel_value, segments=11, warmup=1):
             drv.do_filter()
         q.sync()
         settle(lambda: ops.fir(taps_d, probe_x, D, probe_n, out=probe_out, am=True), SETTLE_S)
-        # outputs delivered in the timed steps: the Fir's outputs consumed minus what still waits in
-        # the AM window (unfused steps need not line up with segments)
+        # outputs through the WHOLE chain in the timed steps: the fewer of the FIR outputs computed
+        # and the AM outputs computed in them. Unfused, the Fir fills the AM window ahead by its
+        # headroom (2-3 segments per launch), so the AM stage alone also drains what the Fir computed
+        # during warm-up; r03 counted those AM outputs and credited the timed steps with FIR work
+        # done before them (583 Gs/s "unfused" > the kernel line: 3 FIR launches of ~60 M outputs
+        # in 10 timed steps, rocprof trace profiles/r04/exp/nodes_trace_summary.txt)
         fir0, am0 = fir.output_size()[0] // 8, am.output_size()[0] // 4
         t0 = time.perf_counter()
         for _ in range(steps):
             drv.do_filter()
         q.sync()
         dt = (time.perf_counter() - t0) / steps
-        done = (fir0 - fir.output_size()[0] // 8) - (am.output_size()[0] // 4 - am0)
+        fir_done = fir0 - fir.output_size()[0] // 8           # FIR outputs computed (Fir input consumed)
+        am_done = fir_done - (am.output_size()[0] // 4 - am0)  # AM outputs computed (AM input consumed)
+        done = min(fir_done, am_done)
         msps = done * D / steps / dt / 1e6
         st = drv.graph_stats()
         key = "fused" if fuse else "unfused"
         out[key] = {"value": msps, "unit": "Msamples/s", "ms_per_step": dt * 1e3,
-                    "outputs_per_step": done / steps, "fused_edges": st["fused"],
+                    "outputs_per_step": done / steps, "fir_outputs": fir_done, "am_outputs": am_done,
+                    "fused_edges": st["fused"],
                     "vs_kernel_line": msps / kernel_value}
         del drv, sink, am, fir
         torch.cuda.empty_cache()

@@ -52,7 +52,26 @@ namespace fftfir {
 // gsdrAmdFftDirectBlocks; one vector atomic per fallback block).
 __device__ unsigned long long gDirectBlocks;
 
-constexpr int kM = 512;       // FFT points per phase per block
+// In-kernel clock stamps, diagnostic builds only (tools/exp/run_fft_variants.sh stamps; the product
+// build compiles none): per wave of the first 256 workgroups, the shader-clock and the 100 MHz
+// real-time counters after the prologue and after the wave's last block, so the clock the kernel
+// runs at is read inside it (MI355X_MICROARCH.md, DVFS give-back item 6). The stamps go to this
+// array only; nothing in the kernel reads them.
+#ifndef GSDR_FFT_STAMPS
+#define GSDR_FFT_STAMPS 0
+#endif
+// Attribution switches, diagnostic builds only (0 in the product build: every test below folds away):
+// bit 1 no FFT math, 2 no global loads (synthetic rows), 4 no LDS transposition, 8 no accuracy
+// guard, 16 no output stores.
+#ifndef GSDR_FFT_EXP
+#define GSDR_FFT_EXP 0
+#endif
+#if GSDR_FFT_STAMPS
+constexpr int kStampWaves = 256 * 8;
+__device__ unsigned long long gFftStamps[kStampWaves * 4];
+#endif
+
+constexpr int kM = 512;      // FFT points per phase per block
 constexpr int kWaves = 8;     // waves per workgroup (one workgroup per CU)
 constexpr int kThreads = kWaves * kWave;
 constexpr int kSA = 10;       // pattern-A exchange row stride (complex): see exchangeA
@@ -480,12 +499,14 @@ __device__ __forceinline__ void loadRows(const Args& a, int64_t b, Rows<D, kCf32
       // (the previous block's tail) and 6-7 (re-read by the next block) keep the default policy so
       // the overlap stays an L2 hit. C3 490 -> 485 us, profiles/r03/exp/fft_nt_mid_ab.log
       const int off = ((j * D / 2 + i) * 64 + l) * 16;
-      const f4 u = ((GSDR_FFT_NT_GROUPS >> j) & 1) ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2))
-                                                   : __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      const f4 u = (GSDR_FFT_EXP & 2) ? f4{(float)(l + i), (float)j, (float)(b & 7), 1.0f}
+                   : ((GSDR_FFT_NT_GROUPS >> j) & 1) ? __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2))
+                                                     : __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       R.v[j][2 * i] = f2{u.x, u.y};
       R.v[j][2 * i + 1] = f2{u.z, u.w};
     }
   }
+  if (GSDR_FFT_EXP & 4) return;
   transposeRows<D>(R, s, l);
 }
 
@@ -629,7 +650,7 @@ __device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& 
     for (int n = 0; n < NP; ++n)
 #pragma unroll
       for (int j = 0; j < 8; ++j) z[n][j] = (MIX && IN == kI8) ? cmul(R.point(j, p + n), t[j]) : R.point(j, p + n);
-    fftFwd<NP>(z, L, l);
+    if (!(GSDR_FFT_EXP & 1)) fftFwd<NP>(z, L, l);
 #pragma unroll
     for (int n = 0; n < NP; ++n) {
       f2 g[8], u[8];
@@ -645,7 +666,7 @@ __device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& 
       for (int d = 0; d < 8; ++d) acc[0][d] = cmul2(z[n][d], g[d], u[d]);
     }
   }
-  ifft512(acc, L, l);
+  if (!(GSDR_FFT_EXP & 1)) ifft512(acc, L, l);
   if constexpr (MIX && EPI != kAm) {  // the block's factor E_b (|E_b y| = |y|: AM needs none)
     const f2 eb = turnExpF(a.mixPhase0 + (uint64_t)(b * (int64_t)a.V * D) * a.mixStep);
 #pragma unroll
@@ -660,7 +681,7 @@ __device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& 
 #pragma unroll
   for (int h = 0; h < 8; ++h) {
     const int m = l + 64 * h;
-    if (m < nv) {
+    if (m < nv && !((GSDR_FFT_EXP & 16) && a.T > 0)) {
       if (EPI == kAm)
         (reinterpret_cast<float*>(a.out) + k0)[m] = amEnvelope(acc[0][h]);
       else
@@ -680,6 +701,9 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   L.tw = reinterpret_cast<const f4*>(twAll) + l;
   L.scratch = twAll + kTw + w * scratchComplex<D>(IN);
   buildTables<D, IN, kWaves, MIX>(a, twAll, L, w, l, mixT);
+#if GSDR_FFT_STAMPS
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // round r: workgroup g's wave w takes block (r * groups + g) * kWaves + w, so in every round
   // the grid streams one contiguous stretch of the input (DRAM-friendly, like a grid-stride copy)
@@ -698,7 +722,7 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
           for (int p = 0; p < D; ++p) R.v[j][p] = cmul(R.v[j][p], t[j]);
       }
     }
-    if (blockNeedsDirect<D, IN>(a, R, b, l)) {
+    if (!(GSDR_FFT_EXP & 8) && blockNeedsDirect<D, IN>(a, R, b, l)) {
       if (l == 0) atomicAdd(&gDirectBlocks, 1ull);
       directBlock<D, IN, EPI, MIX>(a, b, l);
       continue;
@@ -713,6 +737,17 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
     convolveBlock<D, IN, EPI, MIX>(a, R, b, L, l, t);
     __builtin_amdgcn_s_setprio(0);
   }
+#if GSDR_FFT_STAMPS
+  const unsigned long long st1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+  const int slot = (int)blockIdx.x * kWaves + w;
+  if (l == 0 && slot < kStampWaves) {
+    unsigned long long* s = gFftStamps + 4 * slot;
+    s[0] = st0;
+    s[1] = rt0;
+    s[2] = st1;
+    s[3] = rt1;
+  }
+#endif
 }
 
 // ---- one wave per SIMD with the next block's loads in flight (D = 1) ---------------------------
@@ -1072,6 +1107,14 @@ hipError_t launchFft(fftfir::Args a, size_t D, hipStream_t stream) {
 }
 
 }  // namespace
+
+#if GSDR_FFT_STAMPS
+// Diagnostic builds: the stamps of the last firFftKernel launch (4 per wave, kStampWaves waves).
+hipError_t fftStampsRead(unsigned long long* host, size_t count) {
+  if (count > (size_t)fftfir::kStampWaves * 4) count = (size_t)fftfir::kStampWaves * 4;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(fftfir::gFftStamps), count * sizeof(unsigned long long));
+}
+#endif
 
 // Eligible: real taps (FC), D in {2,4,6,8,10}, enough taps that the FFT beats the direct forms,
 // at least 64 outputs per block, and the loads' alignment (cf32: 16-byte input; int8 IQ: 4-byte).

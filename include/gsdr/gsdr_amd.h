@@ -176,6 +176,10 @@ GSDR_API hipError_t gsdrAmdWsAborts(int32_t device, uint64_t* count, int reset);
  * gets an abort reported by its next call, and the common case costs no API call. */
 GSDR_API uint32_t gsdrAmdWsTakeAborts(int32_t device);
 GSDR_API uint32_t gsdrAmdWsAbortsPending(int32_t device);
+/* Build provenance: 16 hex digits of the sha256 over the sources this library was built from
+ * (tools/source_hash.py: kernels, runtime, C API, public headers, Makefile). A library that does not
+ * match the tree it is tested with fails tests/test_abi_exports.py. */
+GSDR_API const char* gsdrAmdBuildId(void);
 
 GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
                                     uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,

@@ -83,3 +83,33 @@ int main() { CudaDevicePushPop p(0); (void)p; return 0; }
                         "-I/opt/rocm/include", "-I" + os.path.join(REPO, "include"), str(src)],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
+
+
+def _library_build_id(path):
+    code = ("import ctypes,sys; L=ctypes.CDLL(sys.argv[1]); f=L.gsdrAmdBuildId; "
+            "f.restype=ctypes.c_char_p; print(f().decode())")
+    r = subprocess.run([sys.executable, "-c", code, path], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.strip()
+
+
+def _check_build_id(path):
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from source_hash import source_hash
+    tree = source_hash(REPO)
+    lib_id = _library_build_id(path)
+    assert lib_id == tree, (f"{path} was built from other sources (build id {lib_id}) than this tree "
+                            f"({tree}): rebuild it (make -C cuda-sdr_amd) before testing")
+
+
+def test_library_matches_source_tree(built):
+    """Build provenance: the library's embedded source hash equals the tree's."""
+    _check_build_id(built)
+
+
+@pytest.mark.gpu
+def test_gpu_box_library_matches_source_tree():
+    """The same check where the GPU suite runs: the pushed, prebuilt .so the box loads must be the one
+    built from the tree it runs with, so a stale library fails loudly instead of passing the suite."""
+    assert os.path.exists(LIB), LIB
+    _check_build_id(LIB)

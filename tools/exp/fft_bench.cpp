@@ -22,10 +22,12 @@
   uint32_t kernelPolicy() { return 0; }                                                              \
   bool firI8MfmaEligible(size_t, size_t, const void*) { return false; }                              \
   bool firI8DecMfmaEligible(size_t, size_t, const void*) { return false; }                           \
+  hipError_t fftStampsRead(unsigned long long*, size_t) __attribute__((weak));                         \
   }
 VARIANT_DECLS
 
 typedef hipError_t (*LaunchFn)(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t);
+typedef hipError_t (*StampFn)(unsigned long long*, size_t);
 
 // two tones like bench.py's synthetic C3 input (gsdrSynthWidebandCf32: exp(j 2 pi f1 n) +
 // 0.5 exp(j 2 pi f2 n) + noise), selected with FFT_BENCH_DATA=twotone
@@ -207,7 +209,7 @@ int main() {
   struct Shape { const char* name; size_t n, T, D; bool i8; } shapes[] = {{"c3", (1u << 28) - 6, 1023, 10, false},
                                                                           {"c5rf", 125000000, 1023, 10, true},
                                                                           {"c4", (1u << 27), 1023, 1, false}};
-  struct V { const char* name; LaunchFn fn; } vars[] = {VARIANT_TABLE};
+  struct V { const char* name; LaunchFn fn; StampFn stamps; } vars[] = {VARIANT_TABLE};
   const int nv = sizeof(vars) / sizeof(vars[0]);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -241,6 +243,58 @@ int main() {
     }
     hipMemcpy(taps, ht.data(), sh.T * 4, hipMemcpyHostToDevice);
     if (!sh.i8 && getenv("FFT_BENCH_READBW")) readBw(x, inBytes);
+    // FFT_BENCH_STAMPS=1 (variants built with STAMPS=1): per variant, FFT_BENCH_STAMP_S seconds of
+    // back-to-back launches (default 2.5), then the in-kernel clock of the last launch from its wave
+    // stamps: (shader-clock delta) / (100 MHz real-time delta) per wave, median over waves
+    // (MI355X_MICROARCH.md DVFS give-back item 6). Two interleaved rounds.
+    if (getenv("FFT_BENCH_STAMPS")) {
+      if (sh.i8 || sh.D == 1) { hipFree(x); hipFree(taps); hipFree(out); hipFree(ref); continue; }
+      const double secs = getenv("FFT_BENCH_STAMP_S") ? atof(getenv("FFT_BENCH_STAMP_S")) : 2.5;
+      std::vector<unsigned long long> st(256 * 8 * 4);
+      for (int rd = 0; rd < 2; ++rd)
+        for (int v = 0; v < nv; ++v) {
+          if (!vars[v].stamps) { printf("%s: no stamps in this build (STAMPS=1)\n", vars[v].name); continue; }
+          double el = 0.0, lastUs = 0.0;
+          int launches = 0;
+          while (el < secs * 1e3) {
+            hipEventRecord(e0);
+            for (int r = 0; r < 200; ++r) vars[v].fn(x, sh.i8, taps, sh.T, sh.D, out, nOut, 2, 0);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            el += ms;
+            launches += 200;
+            lastUs = ms * 1e3 / 200;
+          }
+          hipDeviceSynchronize();
+          std::fill(st.begin(), st.end(), 0ull);
+          vars[v].stamps(st.data(), st.size());
+          std::vector<double> clk, dur, start;
+          unsigned long long rtMin = ~0ull;
+          for (int wv = 0; wv < 256 * 8; ++wv)
+            if (st[4 * wv + 3] > st[4 * wv + 1]) rtMin = std::min(rtMin, st[4 * wv + 1]);
+          for (int wv = 0; wv < 256 * 8; ++wv) {
+            const unsigned long long* q = &st[4 * wv];
+            if (q[3] <= q[1] || q[2] <= q[0]) continue;
+            clk.push_back((double)(q[2] - q[0]) / (double)(q[3] - q[1]) * 100.0);  // MHz
+            dur.push_back((double)(q[3] - q[1]) * 0.01);                           // us
+            start.push_back((double)(q[1] - rtMin) * 0.01);
+          }
+          if (clk.empty()) { printf("%s: no stamps read\n", vars[v].name); continue; }
+          std::sort(clk.begin(), clk.end());
+          std::sort(dur.begin(), dur.end());
+          std::sort(start.begin(), start.end());
+          printf("stamps %-10s round %d: %d launches in %.2f s, last 200 at %.1f us/launch | clock MHz median %.0f "
+                 "[p10 %.0f, p90 %.0f] over %zu waves | wave span us median %.1f [min %.1f, max %.1f] | start skew "
+                 "max %.1f us\n",
+                 vars[v].name, rd, launches, el * 1e-3, lastUs, clk[clk.size() / 2], clk[clk.size() / 10],
+                 clk[clk.size() * 9 / 10], clk.size(), dur[dur.size() / 2], dur[0], dur.back(), start.back());
+          fflush(stdout);
+        }
+      hipFree(x); hipFree(taps); hipFree(out); hipFree(ref);
+      continue;
+    }
     // FFT_BENCH_LOOP=<variant name>: loop that variant for FFT_BENCH_REPS launches (power / clock
     // probes sample amd-smi meanwhile), printing the mean launch time every 2000 launches
     if (const char* lv = getenv("FFT_BENCH_LOOP")) {

@@ -2,14 +2,14 @@
 # Build (here) and run (on the GPU box) attribution variants of csrc/kernels/fir_fft.hip.
 #   bash tools/exp/run_fft_variants.sh build   # CPU container
 #   bash tools/exp/run_fft_variants.sh run     # GPU box
-# GSDR_FFT_EXP bits: 1 no FFT math, 2 no global loads, 4 no LDS transposition, 8 no guard,
-# 16 no stores. An optional third field names another source file (e.g. a saved baseline).
+# GSDR_FFT_EXP bits (in the kernel source, 0 in the product build): 1 no FFT math, 2 no global
+# loads, 4 no LDS transposition, 8 no guard, 16 no stores. STAMPS=1 builds every variant with the
+# in-kernel clock stamps (GSDR_FFT_STAMPS; run with FFT_BENCH_STAMPS=1). An optional third field
+# names another source file (e.g. a saved baseline).
 set -eu
 cd "$(dirname "$0")/../.."
 OUT=tools/exp/_build_fft
 KSRC=cuda-sdr_amd/csrc/kernels/fir_fft.hip
-# the attribution switches live in a patch, applied to a copy (the shipped kernel has none)
-ASRC=${OUT:-tools/exp}/fir_fft_attr.hip
 VARIANTS=${VARIANTS:-"base|
 nofft|-DGSDR_FFT_EXP=1
 noload|-DGSDR_FFT_EXP=2
@@ -17,20 +17,18 @@ notrans|-DGSDR_FFT_EXP=4
 noguard|-DGSDR_FFT_EXP=8
 nostore|-DGSDR_FFT_EXP=16
 fft_only|-DGSDR_FFT_EXP=30
-
-
-
 load_only|-DGSDR_FFT_EXP=29"}
+STAMPFLAG=""
+[ "${STAMPS:-0}" = 1 ] && STAMPFLAG="-DGSDR_FFT_STAMPS=1"
 if [ "${1:-build}" = build ]; then
   mkdir -p $OUT
-  patch -s -o $ASRC $KSRC tools/exp/attribution/fir_fft.patch || echo "attribution patch does not apply to the current kernel (variants naming a source still build)"
   decls=""; table=""; objs=""; i=0
   while IFS='|' read -r name flags src; do
     [ -z "$name" ] && continue
     hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Iinclude -Icuda-sdr_amd/csrc/kernels \
       -Dgsdr_amd=f$i -DgsdrAmdSetFftGuard=f${i}_sg -DgsdrAmdGetFftGuard=f${i}_gg -DgsdrAmdFftDirectBlocks=f${i}_db \
-      $flags -c ${src:-$ASRC} -o $OUT/f$i.o &
-    decls="$decls DECL($i)"; table="$table {\"$name\", f$i::launchPlain},"; objs="$objs $OUT/f$i.o"
+      $STAMPFLAG $flags -c ${src:-$KSRC} -o $OUT/f$i.o &
+    decls="$decls DECL($i)"; table="$table {\"$name\", f$i::launchPlain, f$i::fftStampsRead},"; objs="$objs $OUT/f$i.o"
     i=$((i+1))
   done <<< "$VARIANTS"
   wait
