@@ -475,14 +475,16 @@ def kernel_name(chain):
 
 
 def load_traffic(wl):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    """(HBM bytes per launch, where that figure was measured) of the dominant kernel from the
+    committed rocprofv3 PMC summary profiles/pmc_traffic.json."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(wl, {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get(wl, {})
+        return e.get("hbm_bytes_per_launch"), ({"kernel": e.get("kernel"), "launches": e.get("launches"),
+                                                "note": e.get("note")} if e else None)
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
 def _free_port():
@@ -595,6 +597,75 @@ def mixed_vs_plain(ops, chain, reps=10):
             "plain_ms": plain, "mixed_ms": mixed, "mixed_over_plain": mixed / plain}
 
 
+def host_fed_c5(device, slots=4, warmup=8, steps=48):
+    """C5 fed from host memory (north_star: src/buffers -> pinned hipHostMalloc ring buffers;
+    the reference's ingest CudaMemcpyFilter.cpp:28-104): the gsdrAmChain executor with a ring of
+    `slots` pinned input / output slots of one 5 M-sample chunk each; per step the chunk's H2D copy
+    runs on the chain's second stream, overlapped with the previous steps' compute, and the audio
+    returns into a pinned output slot. The input slots are filled once (synthetic IQ); every step
+    still copies its 10 MB across PCIe. Reported beside `value` (PCIe-inclusive), never as it."""
+    from gpusdr.chain import AmChain
+    desc, kind, L, T, D, cutoff, window, fs = WORKLOADS["c5"]
+    Ta, Da, cut_a, win_a = C5_AUDIO
+    chain = AmChain(lowpass(T, cutoff, window), D, lowpass(Ta, cut_a, win_a), Da, C5_CHUNK, device.index,
+                    host_slots=slots)
+    from gpusdr import ops
+    for s in range(slots):
+        iq = ops.synth_iq_int8(0x5EED, fs, 1e3, fs * 0.075, s * C5_CHUNK, C5_CHUNK, device=device)
+        chain.host_input(s)[:] = iq.cpu().numpy()
+    counts = [0] * slots
+    audio = 0
+
+    def run(n, first):
+        nonlocal audio
+        for k in range(first, first + n):
+            s = k % slots
+            if k >= slots:  # the slot's previous step must be done before it is refilled / reused
+                audio += len(chain.wait_host(s, counts[s]))
+            counts[s] = chain.step_host(s)
+
+    run(warmup, 0)
+    torch.cuda.synchronize()
+    audio = 0
+    t0 = time.perf_counter()
+    run(steps, warmup)
+    for k in range(warmup + steps - slots, warmup + steps):
+        audio += len(chain.wait_host(k % slots, counts[k % slots]))
+    dt = time.perf_counter() - t0
+    chain.close()
+    msps = steps * C5_CHUNK / dt / 1e6
+    return {"workload": f"C5 fed from host memory: {slots} pinned hipHostMalloc slots of {C5_CHUNK} int8 IQ samples, "
+                        "H2D on the chain's copy stream overlapped with compute, audio back into pinned slots",
+            "value": msps, "unit": "Msamples/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
+            "h2d_gbs": msps * 2e6 / 1e9, "audio_samples": audio,
+            "note": "PCIe-inclusive rate, reported beside value (inputs resident in HBM), never as it"}
+
+
+def hbm_probe(ops, device, nbytes=2 << 30, reps=10):
+    """Measured HBM bandwidth in this process (% of spec AND of measured copy BW):
+    gsdrAmdHbmProbe streaming-read (float4 loads, one sum per thread) and copy kernels over `nbytes`
+    buffers, HIP events around `reps` launches after two warm-ups; GB/s of bytes moved (copy:
+    read + write)."""
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=device).fill_(1.0)
+    dst = torch.empty_like(src)
+    res = {}
+    for mode, name, moved in ((0, "read", nbytes), (1, "copy", 2 * nbytes)):
+        for _ in range(2):
+            ops.hbm_probe(src, dst, mode)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            ops.hbm_probe(src, dst, mode)
+        b.record()
+        b.synchronize()
+        ms = a.elapsed_time(b) / reps
+        res[name + "_gbs"] = moved / (ms * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    res["bytes"] = nbytes
+    return res
+
+
 def node_path(ops, device, kernel_value, segments=11, warmup=1):
     """C3 through the reference's filter-graph API (getFactoriesSingleton nodes, SteppingDriver):
     Fir(real taps, FloatComplex, D = 10) -> QuadAmDemod -> a device sink taking one C3 segment of AM
@@ -664,7 +735,17 @@ def node_path(ops, device, kernel_value, segments=11, warmup=1):
                     "vs_kernel_line": msps / kernel_value}
         del drv, sink, am, fir
         torch.cuda.empty_cache()
-    # host cost of a driver step at the reference's 1 MiB chunk: eager vs graph replay
+    out["host_step_1MiB"] = host_step_costs(ops, device)
+    return out
+
+
+def host_step_costs(ops, device, steps=60):
+    """Host time of one SteppingDriver step of the fused C3 chain (Fir -> QuadAmDemod -> device
+    sink) at the reference's 1 MiB chunk: doFilter (eager) vs doFilterGraphed (replay), medians of
+    the second half of `steps` pushes."""
+    from gpusdr import graph
+    desc, kind, L, T, D, cutoff, window, fs = WORKLOADS["c3"]
+    taps = lowpass(T, cutoff, window)
     q = graph.Queue(device.index)
     chunk = 131_070  # cf32 samples, a multiple of D: the chain's state repeats
     xs = torch.empty(chunk, dtype=torch.complex64, device=device)
@@ -678,15 +759,14 @@ def node_path(ops, device, kernel_value, segments=11, warmup=1):
         drv.connect(fir, 0, am, 0)
         drv.connect(am, 0, sink, 0)
         ts = []
-        for i in range(60):
+        for i in range(steps):
             fir.push_device(xs.data_ptr(), chunk * 8)
             t0 = time.perf_counter()
             drv.do_filter() if mode == "eager" else drv.do_filter_graphed(q)
             ts.append(time.perf_counter() - t0)
             q.sync()
-        host[mode] = {"host_us_per_step": float(np.median(ts[30:])) * 1e6, **drv.graph_stats()}
-    out["host_step_1MiB"] = host
-    return out
+        host[mode] = {"host_us_per_step": float(np.median(ts[steps // 2:])) * 1e6, **drv.graph_stats()}
+    return host
 
 
 def main():
@@ -754,22 +834,29 @@ def main():
             torch.cuda.empty_cache()
         if world == 1:
             extras["c3_nodes"] = node_path(ops, device, value)
+            extras["c5_host_fed"] = host_fed_c5(device)
         chain = argparse.Namespace(kernel_class=chain_info[0], L=chain_info[2], T=chain_info[3], D=chain_info[4],
                                    kind=chain_info[5], geom=chain_info[6], n_slots=chain_info[7])
         kernel_label = chain_info[1]
     else:
         kernel_label = kernel_name(chain)
+    # measured bandwidth in this process, the second reference of the roofline
+    probe = hbm_probe(ops, device) if not args.no_extras else None
 
     if rank == 0:
         desc = WORKLOADS[args.workload][0]
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.workload)
-        traffic = load_traffic(args.workload)
+        traffic, traffic_src = load_traffic(args.workload)
         rf_traffic = None
         if args.workload == "c5" and not (world == 1 and args.c5_mode == "sharded"):
             # the PMC summary is of the fused N = 1 step's one launch; elsewhere the timed region
-            # holds more launches (bulk + head, or an executor graph)
+            # holds more launches (bulk + head, or an executor graph): kept apart, labelled by source
+            rf_traffic, traffic = traffic, None
+        if world > 1 and traffic is not None:
+            # profiled at N = 1 (one launch over the whole step); at N > 1 the timed launch is the bulk
+            # part, a different size: the per-launch figure is that configuration's, labelled
             rf_traffic, traffic = traffic, None
         line = {
             "metric": METRIC,
@@ -809,7 +896,11 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
-                **({"traffic_fused_rf_audio_kernel": rf_traffic} if rf_traffic is not None else {}),
+                **({"traffic_of_profiled_config": rf_traffic} if rf_traffic is not None else {}),
+                "traffic_source": traffic_src,
+                **({"measured_read_gbs": probe["read_gbs"], "measured_copy_gbs": probe["copy_gbs"],
+                    "frac_of_measured_read": achieved_gbs / probe["read_gbs"],
+                    "frac_of_measured_copy": achieved_gbs / probe["copy_gbs"]} if probe else {}),
                 "avg_launch_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": bytes_,
                 "compute": {"kind": compute_kind, "achieved_tflops": achieved_t, "peak_tflops": peak_t,

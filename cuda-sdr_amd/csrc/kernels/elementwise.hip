@@ -178,7 +178,41 @@ __global__ __launch_bounds__(kBlock) void synthWideband(uint64_t seed, double f1
 
 using namespace gsdr_amd;
 
+// ---- HBM bandwidth probe (diagnostics: the measured read / copy bandwidth the bench reports the
+// roofline against, beside the 8 TB/s spec) -------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void hbmProbeKernel(const f4* __restrict__ in, f4* __restrict__ out, size_t n4) {
+  float acc = 0.0f;
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (size_t)gridDim.x * kBlock) {
+    const f4 v = in[i];
+    if (MODE == 1) out[i] = v;
+    else acc += v.x + v.y + v.z + v.w;
+  }
+  // read mode: the sum must look used; it is never equal to this for finite data of the probe
+  if (MODE == 0 && acc == -1.2345e-38f) out[0] = f4{acc, acc, acc, acc};
+}
+
 extern "C" {
+
+hipError_t gsdrAmdHbmProbe(const void* input, void* output, size_t bytes, int32_t mode, int32_t device,
+                           hipStream_t stream) {
+  if (bytes < 16 || input == nullptr || output == nullptr || !aligned16(input) || !aligned16(output) ||
+      (mode != 0 && mode != 1))
+    return hipErrorInvalidValue;
+  DevicePush push(device);
+  if (!push.ok) return hipErrorInvalidDevice;
+  const size_t n4 = bytes / 16;
+  int n = 256;
+  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device);
+  const dim3 grid((unsigned)(n * 8));  // 8 blocks of 256 per CU: the grid-stride sweep's best (fft_bench readBw)
+  if (mode == 0)
+    hipLaunchKernelGGL(hbmProbeKernel<0>, grid, dim3(kBlock), 0, stream, reinterpret_cast<const f4*>(input),
+                       reinterpret_cast<f4*>(output), n4);
+  else
+    hipLaunchKernelGGL(hbmProbeKernel<1>, grid, dim3(kBlock), 0, stream, reinterpret_cast<const f4*>(input),
+                       reinterpret_cast<f4*>(output), n4);
+  return hipGetLastError();
+}
 
 hipError_t gsdrInt8ToNormFloat(const int8_t* input, float* output, size_t numElements, int32_t device,
                                hipStream_t stream) {

@@ -762,6 +762,14 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
       return launchFirFft(in, INK == kInI8IQ, taps, tapCount, decimation, out, nOut, EPI, stream,
                           FftMix{mix.on, mix.phase0, mix.step});
   }
+  // long complex-tap filters on cf32 (gsdrFirCC / gsdrFirCCAmDemod): the same FFT kernels, whose filter
+  // spectra are complex anyway (G_p = conj(DFT(conj h_p)) / M): 8 T / D direct-form flops per sample
+  // become the FC path's FFT work
+  if constexpr (MODE == kFirCC && INK == kInCF32 && (EPI == kEpiComplex || EPI == kEpiAm)) {
+    if (!mix.on && (kernelPolicy() & (GSDR_POLICY_NO_FFT | GSDR_POLICY_NO_MFMA)) == 0 &&
+        firFftEligible(tapCount, decimation, in, false, false))
+      return launchFirFft(in, false, taps, tapCount, decimation, out, nOut, EPI, stream, FftMix{}, true);
+  }
   // int8 IQ with real taps: the exact int8 MFMA kernel when the shape allows it (the matrix-core
   // kernels take unmixed samples: a mixed stream is no longer integer)
   if constexpr (MODE == kFirFC && INK == kInI8IQ && EPI != kEpiPair && EPI != kEpiFm) if (!mix.on) {

@@ -662,6 +662,22 @@ struct WsCtl {
 };
 constexpr int kWsCtlZeroWords = (int)(offsetof(WsCtl, spinLimit) / 4);
 
+// Diagnostic builds only (-DGSDR_WS_DIAG=1, tools/gpu_r04_d.sh; the product build has none): bounds
+// checks on every index the fused audio stage and the AM ring writes compute, counted per kind, to
+// show whether the abort path (a wsWait that returns early) computes an index outside its range -
+// [0] audio-tile waits that returned on an abort, [1] history index outside
+// [0, amH), [2] block-local AM index outside the two ring tiles a window may span, [3] ring write
+// position outside the ring, [4] history reads, [5] ring reads.
+#ifndef GSDR_WS_DIAG
+#define GSDR_WS_DIAG 0
+#endif
+#if GSDR_WS_DIAG
+__device__ unsigned long long gWsDiag[8];
+__device__ __forceinline__ void wsDiag(int kind, bool hit) {
+  if (hit) atomicAdd(&gWsDiag[kind], 1ull);
+}
+#endif
+
 __device__ __forceinline__ void wsSignal(int* p, int lane) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS writes/reads complete
   if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -866,6 +882,9 @@ __device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* pa
       // slot j mod kAmRing is free once the producers finished the audio outputs of tile j - kAmRing + 1
       if (j - kAmRing + 2 > 0) wsWait(c, &c->amFree, kWsProducers * (j - kAmRing + 2));
       const int pos = (j & (kAmRing - 1)) * kCfTileOut + 32 * orow + (lane & 31);
+#if GSDR_WS_DIAG
+      wsDiag(3, pos < 0 || pos >= kAmRing * kCfTileOut);
+#endif
       const float rv = k < a.nOut ? v : 0.0f;
       ring[pos] = rv;
       if (pos < kAmRingMirror) ring[kAmRing * kCfTileOut + pos] = rv;
@@ -1349,6 +1368,7 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 // The lead tile (the previous block's last, computed for the ring only) has no outputs here.
 constexpr int kAudioTapsPerLane = kAudioMaxTaps / 8;
 
+
 __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* ring, WsCtl* c, int t0, bool lead, int t,
                                             int ptid, const float (&ht)[kAudioTapsPerLane]) {
   const int lane = ptid & (kWave - 1);
@@ -1356,6 +1376,9 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
   const int o = lane >> 3, q = lane & 7;
   if (!(lead && t == 0)) {
     wsWait(c, &c->amFull, kCfWaves * (t + 1));
+#if GSDR_WS_DIAG
+    wsDiag(0, lane == 0 && c->abort != 0);
+#endif
     const int64_t g = (int64_t)(t0 + t);
     // smallest j whose window end j aD - amH + aT - 1 is >= X
     auto firstJ = [&](int64_t X) -> int64_t {
@@ -1373,6 +1396,13 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
         // block-local AM index, wrapped once: the mirror behind the ring keeps the window contiguous
         // (immediate-offset LDS reads)
         const float* w = ring + (((int)(k0 - (int64_t)kCfTileOut * t0) + q) & (kAmRing * kCfTileOut - 1));
+#if GSDR_WS_DIAG
+        if (j < jHi) {
+          const int64_t kk0 = k0 - (int64_t)kCfTileOut * t0 + q, kk1 = kk0 + 8 * (kAudioTapsPerLane - 1);
+          wsDiag(2, kk0 < 0 || kk0 < (int64_t)kCfTileOut * (t - 1) || kk1 >= (int64_t)kCfTileOut * (t + 1));
+          wsDiag(5, true);
+        }
+#endif
 #pragma unroll
         for (int u = 0; u < kAudioTapsPerLane; ++u) s = fmaf(ht[u], w[8 * u], s);
       } else {  // windows reaching into the history (the launch's first outputs)
@@ -1384,6 +1414,14 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
         for (int u = 0; u < kAudioTapsPerLane; ++u) {
           const int64_t k = k0 + q + 8 * u;
           float x;
+#if GSDR_WS_DIAG
+          if (j < jHi) {
+            const int64_t kk = k - (int64_t)kCfTileOut * t0;
+            if (k >= 0) wsDiag(2, kk < 0 || kk < (int64_t)kCfTileOut * (t - 1) || kk >= (int64_t)kCfTileOut * (t + 1));
+            else wsDiag(1, a.amH + k < 0 || a.amH + k >= a.amH);
+            wsDiag(k >= 0 ? 5 : 4, true);
+          }
+#endif
           if (k >= 0)
             x = ring[(int)(k - (int64_t)kCfTileOut * t0) & (kAmRing * kCfTileOut - 1)];
           else
@@ -2054,6 +2092,18 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
 }
 
 }  // namespace gsdr_amd
+
+#if GSDR_WS_DIAG
+extern "C" __attribute__((visibility("default"))) hipError_t gsdrAmdWsDiag(unsigned long long* out8, int reset) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(gsdr_amd::gWsDiag), 8 * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[8] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(gsdr_amd::gWsDiag), z, sizeof z);
+  }
+  return e;
+}
+#endif
 
 extern "C" {
 // include/gsdr/gsdr_amd.h: wave-specialised kernel hand-off limit and abort diagnostics.

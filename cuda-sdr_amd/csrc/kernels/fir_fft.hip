@@ -95,7 +95,13 @@ struct Args {
   uint64_t mixPhase0;   // fused frequency shifter (kernels with MIX): sample n of `in` is multiplied
   uint64_t mixStep;     // by exp(j theta(n)), theta(n) = 2 pi (mixPhase0 + n mixStep) / 2^64
   int32_t outAligned;   // `out` is 16-byte aligned (the D = 1 kernel's row-unit stores)
+  int32_t complexTaps;  // taps are {re, im} pairs (gsdrFirCC / gsdrFirCCAmDemod), else real
 };
+
+// Tap j (real taps: imaginary part 0).
+__device__ __forceinline__ f2 tapAt(const Args& a, int j) {
+  return a.complexTaps ? reinterpret_cast<const f2*>(a.taps)[j] : f2{a.taps[j], 0.0f};
+}
 
 // ---- fused frequency shifter -----------------------------------------------------------------------
 // Sample n = (b V + r) D + p of block b (row r, phase p) is multiplied by
@@ -396,7 +402,10 @@ __device__ void buildTables(const Args& a, f2* twAll, const Lds& L, int w, int l
     for (int j = 0; j < 8; ++j) {
       const int q = l + 64 * j;
       const int t = q * D + p;
-      z[0][j] = f2{(q < a.Q && t < a.T) ? a.taps[t] : 0.0f, 0.0f};
+      // the correlation y = sum_q h_p[q] x_p[t + q] has the spectrum X . sum_q h_p[q] W^-qk = X . conj(DFT(conj h_p)):
+      // the FFT of conj(h_p), conjugated below with the scale (real taps: conj h = h)
+      const f2 h = (q < a.Q && t < a.T) ? tapAt(a, t) : f2{0.0f, 0.0f};
+      z[0][j] = f2{h.x, -h.y};
     }
     fftFwd<1>(z, L, l);
     if constexpr (MIX) {  // G_p c_p, the product in double and rounded once
@@ -603,7 +612,7 @@ __device__ void directBlock(const Args& a, int64_t b, int l) {
       const int t1 = t0 + 64 < a.T ? t0 + 64 : a.T;
       float pr = 0.0f, pi = 0.0f;
       for (int t = t0; t < t1; ++t) {
-        const float hv = a.taps[t];
+        const f2 hc = tapAt(a, t);
         float xr, xi;
         if (IN == kCf32) {
           const f2 x = (reinterpret_cast<const f2*>(a.in) + base)[m * D + t];
@@ -619,8 +628,8 @@ __device__ void directBlock(const Args& a, int64_t b, int l) {
           xr = zm.x;
           xi = zm.y;
         }
-        pr = fmaf(hv, xr, pr);
-        pi = fmaf(hv, xi, pi);
+        pr = fmaf(hc.x, xr, fmaf(-hc.y, xi, pr));
+        pi = fmaf(hc.x, xi, fmaf(hc.y, xr, pi));
       }
       re += pr;
       im += pi;
@@ -832,8 +841,9 @@ __device__ void directBlockD1(const Args& a, int64_t b, int l) {
       float pr = 0.0f, pi = 0.0f;
       for (int t = t0; t < t1; ++t) {
         const f2 x = reinterpret_cast<const f2*>(a.in)[k0 + i + t];
-        pr = fmaf(a.taps[t], x.x, pr);
-        pi = fmaf(a.taps[t], x.y, pi);
+        const f2 hc = tapAt(a, t);
+        pr = fmaf(hc.x, x.x, fmaf(-hc.y, x.y, pr));
+        pi = fmaf(hc.x, x.y, fmaf(hc.y, x.x, pi));
       }
       re += pr;
       im += pi;
@@ -1138,9 +1148,10 @@ bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int
 }
 
 hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t tapCount, size_t decimation,
-                        void* out, size_t nOut, int epi, hipStream_t stream, FftMix mix) {
+                        void* out, size_t nOut, int epi, hipStream_t stream, FftMix mix, bool complexTaps) {
   using namespace fftfir;
   if (nOut == 0) return hipSuccess;
+  if (complexTaps && (int8Iq || mix.on)) return hipErrorInvalidValue;
   const size_t D = decimation < 1 ? 1 : decimation;
   if (D == 1) {
     if (int8Iq || mix.on) return hipErrorInvalidValue;
@@ -1158,6 +1169,7 @@ hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t t
     a.inScale = 1.0f;
     a.guardRatio = gFftGuard.load(std::memory_order_relaxed);
     a.outAligned = ((uintptr_t)out & 15) == 0;
+    a.complexTaps = complexTaps ? 1 : 0;
     return epi == kEpiAm ? launchD1<kAm>(a, stream) : launchD1<kComplex>(a, stream);
   }
   Args a{};
@@ -1173,6 +1185,7 @@ hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t t
   a.inRows = (int64_t)(((nOut - 1) * D + tapCount) / D);
   a.inScale = int8Iq ? 1.0f / 127.0f : 1.0f;
   a.guardRatio = gFftGuard.load(std::memory_order_relaxed);
+  a.complexTaps = complexTaps ? 1 : 0;
   const bool am = epi == kEpiAm;
   if (mix.on) {
     a.mixPhase0 = mix.phase0;

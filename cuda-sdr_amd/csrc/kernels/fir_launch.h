@@ -62,7 +62,8 @@ struct FftMix {
 };
 bool firFftEligible(size_t tapCount, size_t decimation, const void* in, bool int8Iq, bool mixed = false);
 hipError_t launchFirFft(const void* in, bool int8Iq, const float* taps, size_t tapCount, size_t decimation,
-                        void* out, size_t nOut, int epi, hipStream_t stream, FftMix mix = FftMix{});
+                        void* out, size_t nOut, int epi, hipStream_t stream, FftMix mix = FftMix{},
+                        bool complexTaps = false);
 
 // Kernel-selection policy bits (gsdrAmdSetKernelPolicy).
 uint32_t kernelPolicy();

@@ -334,8 +334,50 @@ Status SteppingDriver::doSourceOutput(Source* source, Fir* fusedFir) {
 // does not repeat (a tone source's phase) or a node is not on `stream`.
 
 SteppingDriver::~SteppingDriver() {
-  for (const CachedGraph& g : mGraphs) (void)hipGraphExecDestroy(g.exec);
+  for (const CachedGraph& g : mGraphs) {
+    (void)hipGraphExecDestroy(g.exec);
+    (void)hipGraphDestroy(g.graph);
+  }
 }
+
+namespace {
+
+// The kernel launches of a captured step, in order, when its graph is a linear chain of kernel
+// nodes (each node at most one dependency and one dependent); empty otherwise (memcpy / memset nodes,
+// forks): such graphs replay through hipGraphLaunch.
+std::vector<hipKernelNodeParams> linearKernelChain(hipGraph_t graph) {
+  std::vector<hipKernelNodeParams> out;
+  size_t n = 0;
+  if (hipGraphGetNodes(graph, nullptr, &n) != hipSuccess || n == 0 || n > 8) return out;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (hipGraphGetNodes(graph, nodes.data(), &n) != hipSuccess) return out;
+  hipGraphNode_t cur = nullptr;
+  for (hipGraphNode_t v : nodes) {
+    hipGraphNodeType t;
+    size_t deps = 0, dependents = 0;
+    if (hipGraphNodeGetType(v, &t) != hipSuccess || t != hipGraphNodeTypeKernel ||
+        hipGraphNodeGetDependencies(v, nullptr, &deps) != hipSuccess ||
+        hipGraphNodeGetDependentNodes(v, nullptr, &dependents) != hipSuccess || deps > 1 || dependents > 1)
+      return {};
+    if (deps == 0) {
+      if (cur != nullptr) return {};  // two roots: not a chain
+      cur = v;
+    }
+  }
+  while (cur != nullptr) {
+    hipKernelNodeParams p{};
+    if (hipGraphKernelNodeGetParams(cur, &p) != hipSuccess || p.func == nullptr || p.extra != nullptr) return {};
+    out.push_back(p);
+    size_t k = 1;
+    hipGraphNode_t next = nullptr;
+    if (hipGraphNodeGetDependentNodes(cur, &next, &k) != hipSuccess) return {};
+    cur = k == 1 ? next : nullptr;
+  }
+  if (out.size() != n) out.clear();
+  return out;
+}
+
+}  // namespace
 
 bool SteppingDriver::chainState(hipStream_t stream, uint64_t& key) noexcept {
   if (!mStepNodesValid) {  // every connected node, in a fixed order (by address)
@@ -368,6 +410,7 @@ bool SteppingDriver::chainState(hipStream_t stream, uint64_t& key) noexcept {
   uint64_t h = 0xCBF29CE484222325ull ^ (uint64_t)gsdrAmdGetKernelPolicy();
   h = (h ^ guardBits) * 0x100000001B3ull;
   h = (h ^ (uint32_t)gsdrAmdGetWsSpinLimit()) * 0x100000001B3ull;
+  h = (h ^ (mFuseFirAm ? 0x2u : 0x1u)) * 0x100000001B3ull;  // fused and unfused steps capture different work
   for (IGraphStepState* g : mStepNodes) {
     if (g->graphStream() != stream || !g->graphState(h)) return false;
     h = (h ^ reinterpret_cast<uintptr_t>(g)) * 0x100000001B3ull;
@@ -412,7 +455,12 @@ Status SteppingDriver::doFilterGraphed(hipStream_t stream) noexcept {
     for (const CachedGraph& g : mGraphs) {
       if (g.key != key) continue;
       for (const auto& [node, state] : g.post) FWD_IF_ERR(node->restoreStepState(state));
-      SAFE_HIP_OR_RET_STATUS(hipGraphLaunch(g.exec, stream));
+      if (g.kernels.empty()) {
+        SAFE_HIP_OR_RET_STATUS(hipGraphLaunch(g.exec, stream));
+      } else {
+        for (const hipKernelNodeParams& k : g.kernels)
+          SAFE_HIP_OR_RET_STATUS(hipLaunchKernel(k.func, k.gridDim, k.blockDim, k.kernelParams, k.sharedMemBytes, stream));
+      }
       ++mStats.replayed;
       mGraphMisses = 0;
       return Status_Success;
@@ -436,9 +484,9 @@ Status SteppingDriver::doFilterGraphed(hipStream_t stream) noexcept {
     if (graph == nullptr) return Status_RuntimeError;
     hipGraphExec_t exec = nullptr;
     const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
+    if (ie != hipSuccess) (void)hipGraphDestroy(graph);
     SAFE_HIP_OR_RET_STATUS(ie);
-    CachedGraph cg{key, exec, {}};
+    CachedGraph cg{key, exec, graph, linearKernelChain(graph), {}};
     bool saved = true;
     cg.post.reserve(mStepNodes.size());
     for (IGraphStepState* n : mStepNodes) {
@@ -452,6 +500,7 @@ Status SteppingDriver::doFilterGraphed(hipStream_t stream) noexcept {
     } else {
       if (ls == Status_Success) SAFE_HIP_OR_RET_STATUS(hipStreamSynchronize(stream));
       (void)hipGraphExecDestroy(exec);
+      (void)hipGraphDestroy(graph);
     }
     FWD_IF_ERR(ls);
     ++mStats.captured;

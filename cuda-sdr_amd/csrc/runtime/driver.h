@@ -63,6 +63,8 @@ class SteppingDriver final : public ISteppingDriver {
   // stream is stepped together with it - ONE gsdrFirFCAmDemod launch writes |y| straight into the
   // QuadAmDemod's downstream buffer, so the cf32 FIR output never goes through HBM and the AM node's
   // launch disappears (bit-identical output; the AM node's window stays empty). On by default.
+  // Part of the cached graphs' key (chainState): toggling it never replays a step captured in the
+  // other mode.
   void setFuseFirAm(bool on) noexcept { mFuseFirAm = on; }
 
  private:
@@ -113,6 +115,11 @@ class SteppingDriver final : public ISteppingDriver {
   struct CachedGraph {
     uint64_t key;
     hipGraphExec_t exec;
+    hipGraph_t graph;  // kept: `kernels` point into its nodes' parameters
+    // a step that captured as a linear chain of kernel nodes (the steady-state fused Fir -> AM step is
+    // one) is replayed by launching those kernels with their captured parameters: hipGraphLaunch costs
+    // more host time than the one or two launches it replaces
+    std::vector<hipKernelNodeParams> kernels;
     // every node's host state after the captured step, reinstated on replay instead of running
     // the step's host logic again
     std::vector<std::pair<IGraphStepState*, GraphNodeState>> post;

@@ -8,10 +8,12 @@
 //          rank 0: head outputs [0, head) over buf (the halo that arrived last step), then
 //                  `stream` waits for the exchange and copies incoming -> halo for the next step
 //          rank > 0: `stream` waits for the exchange, then the head launch
-// At one rank: a single launch over buf, then the tail is copied into the halo.
+// At one rank: a single launch over buf, then the tail is copied into the halo; or, with an exchange
+// hook, the ring protocol on a ring of one (rank 0's path, the tail sent to itself).
 // The FIR is the reference count rule over [halo | segment] (Fir.cpp:178-186): H + L inputs give
 // exactly L / D outputs because L % D == 0.
 #include <gsdr/gsdr_amd.h>
+#include <gpusdrpipeline/GSLog.h>
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -48,8 +50,15 @@ struct Rccl {
   decltype(&ncclGroupEnd) groupEnd = nullptr;
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGetUniqueId) getUniqueId = nullptr;
+  decltype(&ncclCommInitRank) commInitRank = nullptr;
+  decltype(&ncclCommDestroy) commDestroy = nullptr;
+  decltype(&ncclGetErrorString) errorString = nullptr;
   bool ok = false;
 };
+
+// The calling thread's last RCCL result (gsdrShardRcclLastResult).
+thread_local ncclResult_t tLastResult = ncclSuccess;
 
 const Rccl& rccl() {
   static Rccl r;
@@ -62,9 +71,23 @@ const Rccl& rccl() {
     r.groupEnd = reinterpret_cast<decltype(&ncclGroupEnd)>(dlsym(h, "ncclGroupEnd"));
     r.send = reinterpret_cast<decltype(&ncclSend)>(dlsym(h, "ncclSend"));
     r.recv = reinterpret_cast<decltype(&ncclRecv)>(dlsym(h, "ncclRecv"));
-    r.ok = r.groupStart && r.groupEnd && r.send && r.recv;
+    r.getUniqueId = reinterpret_cast<decltype(&ncclGetUniqueId)>(dlsym(h, "ncclGetUniqueId"));
+    r.commInitRank = reinterpret_cast<decltype(&ncclCommInitRank)>(dlsym(h, "ncclCommInitRank"));
+    r.commDestroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
+    r.errorString = reinterpret_cast<decltype(&ncclGetErrorString)>(dlsym(h, "ncclGetErrorString"));
+    r.ok = r.groupStart && r.groupEnd && r.send && r.recv && r.getUniqueId && r.commInitRank && r.commDestroy &&
+           r.errorString;
   });
   return r;
+}
+
+// Record an RCCL result for the calling thread; a failure is logged with RCCL's text and the call
+// that made it, and becomes hipErrorUnknown for the hipError_t-returning entry points.
+hipError_t ncclStatus(const Rccl& r, ncclResult_t res, const char* what) {
+  tLastResult = res;
+  if (res == ncclSuccess) return hipSuccess;
+  gsloge("%s failed: ncclResult_t %d (%s)", what, (int)res, r.errorString ? r.errorString(res) : "?");
+  return hipErrorUnknown;
 }
 
 }  // namespace
@@ -81,6 +104,9 @@ struct gsdrShardStreamImpl {
   uint8_t* incoming = nullptr;
   hipStream_t xstream = nullptr;
   hipEvent_t segReady = nullptr, exchanged = nullptr;
+  hipEvent_t stepDone = nullptr;  // the last step's completion on its stream (Destroy waits for it)
+  bool stepped = false;
+  bool ring = false;              // the ring protocol (world > 1, or a ring of one with a hook)
   gsdrHaloExchangeFn exchange = nullptr;
   void* user = nullptr;
 
@@ -99,6 +125,7 @@ struct gsdrShardStreamImpl {
   void release() {
     DevicePush push(device);
     if (segReady) (void)hipEventDestroy(segReady);
+    if (stepDone) (void)hipEventDestroy(stepDone);
     if (exchanged) (void)hipEventDestroy(exchanged);
     if (xstream) (void)hipStreamDestroy(xstream);
     (void)hipFree(taps);
@@ -140,17 +167,19 @@ GSDR_API hipError_t gsdrShardStreamCreate(int32_t rank, int32_t world, int32_t i
   s->bulkOffset = s->head * s->D - s->H;  // into the segment: the first input of output `head`
   s->exchange = exchange;
   s->user = user;
+  s->ring = world > 1 || exchange != nullptr;
   hipError_t e = hipMalloc(&s->taps, tapCount * sizeof(float));
   if (e == hipSuccess) e = hipMemcpy(s->taps, taps, tapCount * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&s->buf, (s->H + s->L) * s->elem);
   if (e == hipSuccess) e = hipMemset(s->buf, 0, (s->H + s->L) * s->elem);
-  if (e == hipSuccess && world > 1 && rank == 0 && s->H > 0) {
+  if (e == hipSuccess && s->ring && rank == 0 && s->H > 0) {
     e = hipMalloc(&s->incoming, s->H * s->elem);
     if (e == hipSuccess) e = hipMemset(s->incoming, 0, s->H * s->elem);
   }
-  if (e == hipSuccess && world > 1) e = hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking);
-  if (e == hipSuccess && world > 1) e = hipEventCreateWithFlags(&s->segReady, hipEventDisableTiming);
-  if (e == hipSuccess && world > 1) e = hipEventCreateWithFlags(&s->exchanged, hipEventDisableTiming);
+  if (e == hipSuccess && s->ring) e = hipStreamCreateWithFlags(&s->xstream, hipStreamNonBlocking);
+  if (e == hipSuccess && s->ring) e = hipEventCreateWithFlags(&s->segReady, hipEventDisableTiming);
+  if (e == hipSuccess && s->ring) e = hipEventCreateWithFlags(&s->exchanged, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s->stepDone, hipEventDisableTiming);
   if (e != hipSuccess) {
     s->release();
     delete s;
@@ -163,8 +192,12 @@ GSDR_API hipError_t gsdrShardStreamCreate(int32_t rank, int32_t world, int32_t i
 GSDR_API void gsdrShardStreamDestroy(gsdrShardStream s) {
   if (s == nullptr) return;
   {
+    // no launch or exchange may still use the buffers: the last step's end on its stream (which
+    // waited for the exchange) and the exchange stream itself - not the whole device, which would
+    // stall every other stream of the application
     DevicePush push(s->device);
-    (void)hipDeviceSynchronize();  // no launch may still read the buffers
+    if (s->stepped) (void)hipEventSynchronize(s->stepDone);
+    if (s->xstream) (void)hipStreamSynchronize(s->xstream);
   }
   s->release();
   delete s;
@@ -183,9 +216,11 @@ GSDR_API hipError_t gsdrShardStreamStep(gsdrShardStream s, void* output, hipStre
   auto* out = static_cast<uint8_t*>(output);
   uint8_t* tail = s->buf + s->L * s->elem;  // segment[L - H, L) = buf[L, L + H)
   const size_t haloBytes = s->H * s->elem;
-  if (s->world == 1) {
+  if (!s->ring) {
     SHS_TRY(s->fir(s->buf, s->outputs, out, stream));
     if (haloBytes > 0) SHS_TRY(hipMemcpyAsync(s->buf, tail, haloBytes, hipMemcpyDeviceToDevice, stream));
+    SHS_TRY(hipEventRecord(s->stepDone, stream));
+    s->stepped = true;
     return hipSuccess;
   }
   uint8_t* dst = s->rank == 0 ? s->incoming : s->buf;
@@ -203,6 +238,8 @@ GSDR_API hipError_t gsdrShardStreamStep(gsdrShardStream s, void* output, hipStre
     SHS_TRY(hipStreamWaitEvent(stream, s->exchanged, 0));
     SHS_TRY(s->fir(s->buf, s->head, out, stream));
   }
+  SHS_TRY(hipEventRecord(s->stepDone, stream));
+  s->stepped = true;
   return hipSuccess;
 }
 
@@ -211,11 +248,53 @@ GSDR_API hipError_t gsdrShardExchangeRccl(void* ncclComm, const void* sendTail, 
   const Rccl& r = rccl();
   if (!r.ok) return hipErrorSharedObjectInitFailed;
   auto comm = static_cast<ncclComm_t>(ncclComm);
-  if (r.groupStart() != ncclSuccess) return hipErrorUnknown;
+  SHS_TRY(ncclStatus(r, r.groupStart(), "ncclGroupStart"));
   const ncclResult_t a = r.send(sendTail, bytes, ncclUint8, nextRank, comm, xstream);
   const ncclResult_t b = r.recv(recvHalo, bytes, ncclUint8, prevRank, comm, xstream);
-  const ncclResult_t c = r.groupEnd();
-  return a == ncclSuccess && b == ncclSuccess && c == ncclSuccess ? hipSuccess : hipErrorUnknown;
+  const ncclResult_t c = r.groupEnd();  // always closes the group, even after a failed send / recv
+  SHS_TRY(ncclStatus(r, a, "ncclSend (halo tail)"));
+  SHS_TRY(ncclStatus(r, b, "ncclRecv (halo)"));
+  return ncclStatus(r, c, "ncclGroupEnd (halo exchange)");
+}
+
+GSDR_API hipError_t gsdrShardRcclGetUniqueId(void* uniqueId128) {
+  if (uniqueId128 == nullptr) return hipErrorInvalidValue;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  const Rccl& r = rccl();
+  if (!r.ok) return hipErrorSharedObjectInitFailed;
+  return ncclStatus(r, r.getUniqueId(static_cast<ncclUniqueId*>(uniqueId128)), "ncclGetUniqueId");
+}
+
+GSDR_API hipError_t gsdrShardRcclCommCreate(int32_t nranks, const void* uniqueId128, int32_t rank, int32_t device,
+                                            void** ncclCommOut) {
+  if (ncclCommOut == nullptr || uniqueId128 == nullptr || nranks < 1 || rank < 0 || rank >= nranks)
+    return hipErrorInvalidValue;
+  *ncclCommOut = nullptr;
+  const Rccl& r = rccl();
+  if (!r.ok) return hipErrorSharedObjectInitFailed;
+  DevicePush push(device);
+  if (!push.ok) return hipErrorInvalidDevice;
+  ncclUniqueId id;
+  __builtin_memcpy(&id, uniqueId128, sizeof(id));
+  ncclComm_t comm = nullptr;
+  SHS_TRY(ncclStatus(r, r.commInitRank(&comm, nranks, id, rank), "ncclCommInitRank"));
+  *ncclCommOut = comm;
+  return hipSuccess;
+}
+
+GSDR_API hipError_t gsdrShardRcclCommDestroy(void* ncclComm) {
+  if (ncclComm == nullptr) return hipSuccess;
+  const Rccl& r = rccl();
+  if (!r.ok) return hipErrorSharedObjectInitFailed;
+  return ncclStatus(r, r.commDestroy(static_cast<ncclComm_t>(ncclComm)), "ncclCommDestroy");
+}
+
+GSDR_API int32_t gsdrShardRcclLastResult(const char** message) {
+  if (message != nullptr) {
+    const Rccl& r = rccl();
+    *message = r.errorString ? r.errorString(tLastResult) : "librccl not loaded";
+  }
+  return (int32_t)tLastResult;
 }
 
 }  // extern "C"

@@ -71,6 +71,10 @@ def _declare(L):
     L.gsdrSynthIqInt8.restype = err
     L.gsdrSynthWidebandCf32.argtypes = [u64, f64, f64, u64, vp, sz, i32, vp]
     L.gsdrSynthWidebandCf32.restype = err
+    L.gsdrAmdHbmProbe.argtypes = [vp, vp, sz, i32, i32, vp]
+    L.gsdrAmdHbmProbe.restype = err
+    L.gsdrAmdBuildId.argtypes = []
+    L.gsdrAmdBuildId.restype = ctypes.c_char_p
 
 
 def check(code: int, what: str) -> None:

@@ -29,6 +29,11 @@ def _L():
                 ("gsdrShardStreamHalo", [vp], vp),
                 ("gsdrShardStreamOutputCount", [vp], sz),
                 ("gsdrShardStreamStep", [vp, vp, vp], err),
+                ("gsdrShardRcclGetUniqueId", [vp], err),
+                ("gsdrShardRcclCommCreate", [i32, vp, i32, i32, ctypes.POINTER(vp)], err),
+                ("gsdrShardRcclCommDestroy", [vp], err),
+                ("gsdrShardRcclLastResult", [ctypes.POINTER(ctypes.c_char_p)], i32),
+                ("gsdrShardExchangeRccl", [vp, vp, vp, sz, i32, i32, vp], err),
                 ("hipStreamSynchronize", [vp], err),
                 ("hipMemcpy", [vp, vp, sz, ctypes.c_int], err),
                 ("hipMemcpyAsync", [vp, vp, sz, ctypes.c_int, vp], err)):
@@ -37,6 +42,51 @@ def _L():
             fn.restype = res
         _declared = True
     return L
+
+
+def rccl_last_result():
+    """(ncclResult_t, RCCL's text) of this thread's last RCCL call through the library."""
+    msg = ctypes.c_char_p()
+    code = _L().gsdrShardRcclLastResult(ctypes.byref(msg))
+    return code, (msg.value or b"").decode()
+
+
+def _rccl_check(code, what):
+    if code != 0:
+        res, msg = rccl_last_result()
+        raise RuntimeError(f"{what}: hipError_t {code}, last ncclResult_t {res} ({msg})")
+
+
+class RcclComm:
+    """An RCCL communicator made by the library (gsdrShardRcclCommCreate). Rank 0 calls
+    ``RcclComm.unique_id()`` and hands the 128 bytes to every rank; ``RcclComm(n, uid, rank, device)``
+    on each. Pass it as ShardStream's ``exchange``: the executor then calls gsdrShardExchangeRccl
+    itself (grouped ncclSend / ncclRecv of the halo bytes on its exchange stream; no Python hook)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        _rccl_check(_L().gsdrShardRcclGetUniqueId(buf), "gsdrShardRcclGetUniqueId")
+        return buf.raw
+
+    def __init__(self, nranks: int, uid: bytes, rank: int, device: int = 0):
+        if len(uid) != 128:
+            raise ValueError("an ncclUniqueId is 128 bytes")
+        self._uid = ctypes.create_string_buffer(uid, 128)
+        h = ctypes.c_void_p()
+        _rccl_check(_L().gsdrShardRcclCommCreate(int(nranks), self._uid, int(rank), int(device), ctypes.byref(h)),
+                    "gsdrShardRcclCommCreate")
+        self.handle = h
+
+    def exchange(self, send_tail, recv_halo, nbytes, next_rank, prev_rank, xstream):
+        """gsdrShardExchangeRccl on this communicator (enqueued on `xstream`)."""
+        _rccl_check(_L().gsdrShardExchangeRccl(self.handle, send_tail, recv_halo, nbytes, next_rank, prev_rank,
+                                               xstream), "gsdrShardExchangeRccl")
+
+    def close(self):
+        if self.handle:
+            _rccl_check(_L().gsdrShardRcclCommDestroy(self.handle), "gsdrShardRcclCommDestroy")
+            self.handle = ctypes.c_void_p(None)
 
 
 def host_staged_exchange(group=None):
@@ -82,10 +132,15 @@ class ShardStream:
                 traceback.print_exc()
                 return 999  # hipErrorUnknown
 
-        self._cb = EXCHANGE_FN(trampoline) if exchange is not None else EXCHANGE_FN()
+        user = None
+        if isinstance(exchange, RcclComm):  # the native hook itself, user = the communicator
+            self._cb = ctypes.cast(_L().gsdrShardExchangeRccl, EXCHANGE_FN)
+            user = exchange.handle
+        else:
+            self._cb = EXCHANGE_FN(trampoline) if exchange is not None else EXCHANGE_FN()
         h = ctypes.c_void_p()
         check(_L().gsdrShardStreamCreate(self.rank, self.world, int(self.int8_iq), int(self.am),
-                                         self.taps.ctypes.data, len(self.taps), self.D, self.L, self._cb, None,
+                                         self.taps.ctypes.data, len(self.taps), self.D, self.L, self._cb, user,
                                          self.device, ctypes.byref(h)), "gsdrShardStreamCreate")
         self._h = h
         self.outputs = _L().gsdrShardStreamOutputCount(h)
@@ -107,6 +162,16 @@ class ShardStream:
             raise ValueError(f"expected a contiguous device tensor of {nbytes} bytes")
         stream = torch.cuda.current_stream(x.device)
         check(_L().hipMemcpyAsync(dst, x.data_ptr(), nbytes, _HIP_D2D, stream.cuda_stream), "hipMemcpyAsync")
+
+    @property
+    def halo_ptr(self) -> int:
+        """Device address of the halo (tapCount - 1 samples in front of the segment)."""
+        return _L().gsdrShardStreamHalo(self._h)
+
+    @property
+    def tail_ptr(self) -> int:
+        """Device address of the segment's last tapCount - 1 samples (what the exchange sends on)."""
+        return _L().gsdrShardStreamSegment(self._h) + (self.L - self.halo_samples) * self.elem
 
     def write_segment(self, x: torch.Tensor):
         self._copy_in(_L().gsdrShardStreamSegment(self._h), x, self.L)

@@ -185,6 +185,17 @@ def am_chain_fused(taps: torch.Tensor, iq: torch.Tensor, decimation: int, rf_cou
     return audio_out
 
 
+def hbm_probe(src: torch.Tensor, dst: torch.Tensor, mode: int) -> None:
+    """gsdrAmdHbmProbe: mode 0 streams src (read bandwidth), mode 1 copies src -> dst."""
+    if not (src.is_cuda and dst.is_cuda and src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("contiguous device tensors")
+    n = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < n:
+        raise ValueError("dst too small")
+    check(lib().gsdrAmdHbmProbe(src.data_ptr(), dst.data_ptr(), n, int(mode), _dev(src), _stream(src)),
+          "gsdrAmdHbmProbe")
+
+
 def quad_am_demod(z: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _require(z, torch.complex64, "z")
     if out is None:

@@ -180,6 +180,11 @@ GSDR_API uint32_t gsdrAmdWsAbortsPending(int32_t device);
  * (tools/source_hash.py: kernels, runtime, C API, public headers, Makefile). A library that does not
  * match the tree it is tested with fails tests/test_abi_exports.py. */
 GSDR_API const char* gsdrAmdBuildId(void);
+/* Diagnostics: HBM bandwidth probe over `bytes` (16-byte aligned device buffers): mode 0 streams
+ * `input` (float4 loads, one sum per thread; `output` untouched for finite data), mode 1 copies it to
+ * `output`. The bench times it to report the roofline against measured bandwidth as well as spec. */
+GSDR_API hipError_t gsdrAmdHbmProbe(const void* input, void* output, size_t bytes, int32_t mode, int32_t device,
+                                    hipStream_t stream);
 
 GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
                                     uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,
@@ -284,6 +289,10 @@ GSDR_API hipError_t gsdrAmChainReset(gsdrAmChain chain);
  *   sendTail to nextRank and the receive of `bytes` from prevRank into recvHalo (device).
  * gsdrShardExchangeRccl is such a hook over an RCCL communicator (user = the ncclComm_t; librccl is
  * loaded on first use, one GPU per rank).
+ * With world = 1 and an exchange hook the executor runs the ring protocol on a ring of one (bulk beside
+ * the exchange, head from the halo received one step earlier): the rank sends its tail to itself, as
+ * rank 0 of a G-rank ring receives rank G - 1's (an RCCL self send / receive exercises the whole
+ * protocol on one GPU). Without a hook, world = 1 is one launch plus the history copy.
  *
  * input: int8Iq != 0 -> interleaved int8 IQ (2 bytes per sample), else cf32; output: am != 0 -> the
  * AM envelope (float), else cf32 FIR outputs. L must be a multiple of D and >= T - 1; taps are host
@@ -310,6 +319,17 @@ GSDR_API size_t gsdrShardStreamOutputCount(gsdrShardStream s);
 GSDR_API hipError_t gsdrShardStreamStep(gsdrShardStream s, void* output, hipStream_t stream);
 GSDR_API hipError_t gsdrShardExchangeRccl(void* ncclComm, const void* sendTail, void* recvHalo, size_t bytes,
                                           int32_t nextRank, int32_t prevRank, hipStream_t xstream);
+/* RCCL plumbing for native callers of gsdrShardExchangeRccl (librccl loaded on first use):
+ * GetUniqueId fills the 128-byte ncclUniqueId rank 0 hands to every rank; CommCreate makes this rank's
+ * communicator on `device` (ncclCommInitRank); CommDestroy frees it. When an RCCL call fails, these and
+ * gsdrShardExchangeRccl return hipErrorUnknown (hipErrorSharedObjectInitFailed: librccl missing) and
+ * gsdrShardRcclLastResult returns the calling thread's last ncclResult_t (0 = success) and, through
+ * `message` if non-null, RCCL's text for it; the failure is also logged through gslog. */
+GSDR_API hipError_t gsdrShardRcclGetUniqueId(void* uniqueId128);
+GSDR_API hipError_t gsdrShardRcclCommCreate(int32_t nranks, const void* uniqueId128, int32_t rank, int32_t device,
+                                            void** ncclCommOut);
+GSDR_API hipError_t gsdrShardRcclCommDestroy(void* ncclComm);
+GSDR_API int32_t gsdrShardRcclLastResult(const char** message);
 
 #ifdef __cplusplus
 }

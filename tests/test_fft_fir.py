@@ -93,6 +93,39 @@ def test_fft_fir_matches_float64(ops, orc, kind, T, D, n_out):
     assert direct <= 2, (direct, blocks)
 
 
+CC_CASES = [(1023, 10, 20000), (1023, 10, 1), (600, 6, 3001), (256, 2, 5000), (2000, 8, 999),
+            (1023, 1, 20000), (1023, 1, 3073), (256, 1, 777)]
+
+
+@pytest.mark.parametrize("T,D,n_out", CC_CASES)
+def test_fft_fir_complex_taps(ops, orc, T, D, n_out):
+    """gsdrFirCC / gsdrFirCCAmDemod (Fir.cpp:250-258, complex taps, non-conjugate MAC - SURVEY 8(c))
+    on the FFT kernels: the filter spectra are complex anyway, G_p = conj(DFT(conj h_p)) / M. A
+    complex band-pass (a low-pass shifted by exp(j 2 pi f0 j)) against float64, complex and AM
+    outputs, ordinary data on the FFT (no direct-form blocks), and the direct-form fallback (guard 0)
+    within the same bound."""
+    n_in = (n_out - 1) * D + T
+    x = _signal("c64-noise" if T % 2 else "c64", n_in, T + 3 * D, orc)
+    j = np.arange(T)
+    taps = (orc.lowpass_taps(T, 0.4 / D).astype(np.float64) * np.exp(2j * np.pi * 0.11 / D * j)).astype(np.complex64)
+    taps[T // 3] *= -1.5 + 0.5j
+    x_d, taps_d = _dev(x), _dev(taps)
+    ops.fft_direct_blocks(reset=True)
+    y = _host(ops.fir(taps_d, x_d, D, n_out))
+    am = _host(ops.fir(taps_d, x_d, D, n_out, am=True))
+    assert ops.fft_direct_blocks(reset=True) <= 2
+    y64, bound = orc.fir_f64(taps, x, D, n_out)
+    _check(y, y64, bound, ("fft-cc", T, D, n_out))
+    assert np.all(np.abs(am - np.abs(y64)) <= FIR_TOL * bound + 1e-30), ("fft-cc-am", T, D)
+    prev = ops.set_fft_guard(0.0)  # every block in the direct form
+    try:
+        yd = _host(ops.fir(taps_d, x_d, D, n_out))
+        assert ops.fft_direct_blocks(reset=True) > 0
+    finally:
+        ops.set_fft_guard(prev)
+    _check(yd, y64, bound, ("fft-cc-direct", T, D, n_out))
+
+
 def test_fft_fir_large_stream_properties(ops, orc):
     """2^24-sample C3-shaped stream: a sampled float64 check across the whole range, and the
     FFT result equals the direct forms (MFMA and fp32 VALU kernels) within the same tolerance."""
@@ -144,6 +177,47 @@ def test_fft_fir_full_c3_size(ops, orc):
     bound = np.abs(windows).astype(np.float64) @ np.abs(taps.astype(np.float64))
     err = np.abs(got - np.abs(y))
     assert np.all(err <= FIR_TOL * bound), float(np.max(err / bound))
+
+
+@pytest.mark.parametrize("log2n,am", [(30, True), (27, False)])
+def test_fft_fir_full_c4_size(ops, orc, log2n, am):
+    """BASELINE's C4 at full size on the D = 1 kernel (firFftD1PfKernel): the bench's c4s launch
+    (2^30 cf32 samples = 8 GiB in, 1023 taps, AM: 4 GiB out) and a 2^27-sample complex-output launch.
+    Block b covers outputs [b 8V, (b + 1) 8V), V = 512 - ceil(T / 8) = 384 rows, so 3 072 outputs per
+    block: 4 000 outputs - first and last, both sides of block edges spread over the stream (past 2^31
+    bytes of input and of output, where a 32-bit row or byte index would wrap), the eight output phases
+    of a row and random ones - against float64 on their own windows gathered on the GPU; no block took
+    the direct-form fallback."""
+    import torch
+    T, D = 1023, 1
+    n_in = 1 << log2n
+    n_out = n_in - T + 1
+    x_d = ops.synth_wideband_cf32(0xC4, 0.013, 0.31, 0, n_in)
+    taps = orc.lowpass_taps(T, 0.04, "blackman")
+    taps_d = _dev(taps)
+    assert ops.fir_kernel_class(x_d, taps_d, D) == "fft"
+    ops.fft_direct_blocks(0, reset=True)
+    y_d = ops.fir(taps_d, x_d, D, n_out, am=am)
+    torch.cuda.synchronize()
+    assert ops.fft_direct_blocks(0, reset=True) == 0
+    rng = np.random.default_rng(log2n)
+    per_block = 8 * (512 - -(-T // 8))
+    edges = np.arange(per_block, n_out, per_block * 4099)
+    rows = rng.integers(0, n_out // 8, 16) * 8
+    ks = np.unique(np.concatenate([[0, 1, 7, 8, n_out - 2, n_out - 1], edges - 1, edges,
+                                   (rows[:, None] + np.arange(8)[None, :]).ravel(),
+                                   rng.integers(0, n_out, 4000 - 2 * len(edges) - 134)]))
+    ks = ks[ks < n_out]
+    assert ks.max() * 8 > 1 << 31 or log2n < 28
+    idx = torch.from_numpy(ks).cuda()[:, None] + torch.arange(T, device="cuda")[None, :]
+    windows = x_d[idx].cpu().numpy()
+    got = y_d[torch.from_numpy(ks).cuda()].cpu().numpy()
+    y = windows.astype(np.complex128) @ taps.astype(np.float64)
+    bound = np.abs(windows).astype(np.float64) @ np.abs(taps.astype(np.float64))
+    err = np.abs(got - (np.abs(y) if am else y))
+    assert np.all(err <= FIR_TOL * bound), float(np.max(err / bound))
+    del x_d, y_d
+    torch.cuda.empty_cache()
 
 
 class _Policy:

@@ -39,7 +39,7 @@ def _stream_piece(ops, torch, i8, start, n, dev):
     return x
 
 
-def _rank_main(rank, world, port, case, out_dir):
+def _rank_main(rank, world, port, case, out_dir, transport="host"):
     import sys
     sys.path[:0] = [os.path.join(REPO, "cuda-sdr_amd"), os.path.join(REPO, "oracle")]
     import torch
@@ -47,7 +47,7 @@ def _rank_main(rank, world, port, case, out_dir):
 
     import oracle as orc
     from gpusdr import ops
-    from gpusdr.native_shard import ShardStream, host_staged_exchange
+    from gpusdr.native_shard import RcclComm, ShardStream, host_staged_exchange
 
     i8, am, T, D, L = CASES[case]
     if world > 1:
@@ -58,8 +58,25 @@ def _rank_main(rank, world, port, case, out_dir):
     ops.set_ws_spin_limit(1 << 28)  # several ranks time-share the GPU
     ops.ws_aborts(reset=True)
     taps = orc.lowpass_taps(T, 0.04, "blackman")
-    sh = ShardStream(rank, world, taps, D, L, int8_iq=i8, am=am,
-                     exchange=host_staged_exchange() if world > 1 else None)
+    comm = None
+    if transport == "rccl":  # one communicator of `world` ranks (world 1: a ring of one, self send / recv)
+        torch.cuda.set_device(dev)
+        if world > 1:
+            raise NotImplementedError("RCCL needs one GPU per rank; this box has one")
+        comm = RcclComm(world, RcclComm.unique_id(), rank, 0)
+        # the raw hook first: a byte halo sent to this rank itself arrives intact
+        n = 8190
+        send = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev)
+        recv = torch.zeros(n, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        comm.exchange(send.data_ptr(), recv.data_ptr(), n, rank, rank, torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize()
+        if not torch.equal(send, recv):
+            raise RuntimeError("RCCL self exchange: received bytes differ from the sent ones")
+        exchange = comm
+    else:
+        exchange = host_staged_exchange() if world > 1 else None
+    sh = ShardStream(rank, world, taps, D, L, int8_iq=i8, am=am, exchange=exchange)
     H = T - 1
     if rank == 0:  # the stream's first H samples are the primed history of rank 0's first step
         sh.write_halo(_stream_piece(ops, torch, i8, 0, H, dev))
@@ -74,6 +91,8 @@ def _rank_main(rank, world, port, case, out_dir):
     if aborts:
         raise RuntimeError(f"rank {rank}: {aborts} wave-specialised hand-off aborts")
     sh.close()
+    if comm is not None:
+        comm.close()
     np.save(os.path.join(out_dir, f"{case}_rank{rank}.npy"), np.stack(outs))
     if rank == 0:  # the whole stream as the GPU generates it, for the oracle
         full = _stream_piece(ops, torch, i8, 0, H + world * STEPS * L, dev)
@@ -83,11 +102,7 @@ def _rank_main(rank, world, port, case, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,world", [("c4", 1), ("c4", 2), ("c4", 4), ("c3", 2), ("i8", 1), ("i8", 2)])
-def test_native_shard_stream_matches_oracle(tmp_path, orc, case, world):
-    import torch.multiprocessing as mp
-    mp.start_processes(_rank_main, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True,
-                       start_method="spawn")
+def _check_against_oracle(orc, tmp_path, case, world):
     i8, am, T, D, L = CASES[case]
     per = [np.load(os.path.join(tmp_path, f"{case}_rank{r}.npy")) for r in range(world)]
     got = np.concatenate([per[r][s] for s in range(STEPS) for r in range(world)])
@@ -98,6 +113,88 @@ def test_native_shard_stream_matches_oracle(tmp_path, orc, case, world):
     y64, bound = orc.fir_f64(orc.lowpass_taps(T, 0.04, "blackman"), x, D, n)
     want = np.abs(y64) if am else y64
     err = np.abs(got.astype(np.complex128) - want)
+    assert np.all(err <= FIR_TOL * bound + 1e-30), float(np.max(err / (bound + 1e-30)))
+
+
+@pytest.mark.parametrize("case,world", [("c4", 1), ("c4", 2), ("c4", 4), ("c3", 2), ("i8", 1), ("i8", 2)])
+def test_native_shard_stream_matches_oracle(tmp_path, orc, case, world):
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_main, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    _check_against_oracle(orc, tmp_path, case, world)
+
+
+@pytest.mark.parametrize("case", ["c4", "i8"])
+def test_native_shard_stream_rccl_ring_of_one(tmp_path, orc, case):
+    """the RCCL path executed on the one GPU the box has. In a fresh process the
+    library makes a 1-rank communicator (gsdrShardRcclGetUniqueId / CommCreate), sends a byte halo to
+    itself through gsdrShardExchangeRccl (grouped ncclSend / ncclRecv on a stream) and gets it back
+    intact; then a world-1 ShardStream whose hook IS gsdrShardExchangeRccl runs the ring protocol on a
+    ring of one (bulk launch beside the RCCL transfer on the exchange stream, head from the halo
+    received a step earlier) and must match the float64 oracle. Multi-GPU RCCL stays unmeasured until
+    the driver's 8-GPU node runs it."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_main, args=(1, _free_port(), case, str(tmp_path), "rccl"), nprocs=1, join=True,
+                       start_method="spawn")
+    _check_against_oracle(orc, tmp_path, case, 1)
+
+
+def test_native_shard_async_exchange_two_ranks_one_process(orc):
+    """an exchange that only ENQUEUES its transfers and returns. Two ranks of a
+    2-rank ring live in one process on cuda:0; rank 0's hook puts a ~1 ms spin kernel on its exchange
+    stream, then the two halo copies (its tail -> rank 1's halo, rank 1's tail -> its incoming buffer)
+    and records an event; rank 1's hook makes its exchange stream wait for that event. So the bulk
+    launches run while the halo writes are still pending, rank 1's head must wait on its 'exchanged'
+    event and rank 0 must copy its incoming halo only after the transfer: an ordering bug in the
+    segReady / exchanged events or the rank-0 incoming -> halo copy reads a stale halo and fails the
+    float64 comparison."""
+    import ctypes
+
+    import torch
+
+    from gpusdr import ops
+    from gpusdr.native_shard import ShardStream, _L
+
+    case, world = "c3", 2
+    i8, am, T, D, L = CASES[case]
+    dev = torch.device("cuda", 0)
+    taps = orc.lowpass_taps(T, 0.04, "blackman")
+    H = T - 1
+    ranks = {}
+    done = torch.cuda.Event()
+    lib = _L()
+
+    def hook0(send_tail, recv_halo, nbytes, next_rank, prev_rank, xstream):
+        xs = torch.cuda.ExternalStream(xstream, device=dev)
+        with torch.cuda.stream(xs):
+            torch.cuda._sleep(2_000_000)  # the transfer stays pending while the bulk launches run
+        for dst, src in ((ranks[1].halo_ptr, send_tail), (recv_halo, ranks[1].tail_ptr)):
+            code = lib.hipMemcpyAsync(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 3, ctypes.c_void_p(xstream))
+            if code != 0:
+                raise RuntimeError(f"hipMemcpyAsync {code}")
+        done.record(xs)
+
+    def hook1(send_tail, recv_halo, nbytes, next_rank, prev_rank, xstream):
+        torch.cuda.ExternalStream(xstream, device=dev).wait_event(done)
+
+    ranks[0] = ShardStream(0, world, taps, D, L, int8_iq=i8, am=am, exchange=hook0)
+    ranks[1] = ShardStream(1, world, taps, D, L, int8_iq=i8, am=am, exchange=hook1)
+    ranks[0].write_halo(_stream_piece(ops, torch, i8, 0, H, dev))
+    outs = {0: [], 1: []}
+    for step in range(STEPS):
+        for r in (0, 1):
+            ranks[r].write_segment(_stream_piece(ops, torch, i8, H + (step * world + r) * L, L, dev))
+        ys = [ranks[r].step() for r in (0, 1)]
+        torch.cuda.synchronize()
+        for r in (0, 1):
+            outs[r].append(ys[r].cpu().numpy().copy())
+    for r in (0, 1):
+        ranks[r].close()
+    got = np.concatenate([outs[r][s] for s in range(STEPS) for r in range(world)])
+    x = _stream_piece(ops, torch, i8, 0, H + world * STEPS * L, dev).cpu().numpy()
+    n = world * STEPS * L // D
+    y64, bound = orc.fir_f64(taps, x, D, n)
+    err = np.abs(got.astype(np.complex128) - (np.abs(y64) if am else y64))
     assert np.all(err <= FIR_TOL * bound + 1e-30), float(np.max(err / (bound + 1e-30)))
 
 
