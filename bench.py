@@ -570,7 +570,23 @@ def extra_line(wl, chain, elapsed, kernel_ms, steps, world):
             "scaling": "strong" if strong else "weak", "samples_per_gpu_step": chain.L,
             "kernel": kernel_name(chain), "kernel_class": chain.kernel_class,
             "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS, "avg_launch_ms": kernel_ms,
-            "algorithmic_bytes_per_launch": bytes_}
+            "algorithmic_bytes_per_launch": bytes_,
+            # the unit the kernel computes on (C5's RF stage is MFMA-bound: its HBM frac is not its bound)
+            "compute": {"kind": kind, "achieved_tflops": fl / (kernel_ms * 1e-3) / 1e12, "peak_tflops": peak,
+                        "frac": fl / (kernel_ms * 1e-3) / 1e12 / peak, "flops_per_launch": fl,
+                        "direct_form_flops_per_launch": direct_form_flops(wl, chain)}}
+
+
+def direct_form_flops(wl, chain):
+    """SURVEY 8(d) flop convention: direct-form counts (FC 4 T / D per input sample, FF 2 T / D), i.e.
+    the useful work, against which a padded MFMA or an FFT count can be compared."""
+    if wl == "c5":
+        g = chain.geom
+        n_rf = g.rf_outputs if g is not None else chain.L // chain.D
+        return n_rf * 4 * chain.T + (n_rf // chain.Da) * 2 * chain.Ta
+    g = chain.geom
+    n = g.outputs if chain.single else g.outputs - g.head_outputs  # the timed launch's outputs
+    return n * 4 * chain.T
 
 
 def mixed_vs_plain(ops, chain, reps=10):

@@ -16,9 +16,9 @@
     bool on = false;                                                                                   \
     uint64_t phase0 = 0, step = 0;                                                                     \
   };                                                                                                   \
-  hipError_t launchFirFft(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t, FftMix); \
+  hipError_t launchFirFft(const void*, bool, const float*, size_t, size_t, void*, size_t, int, hipStream_t, FftMix, bool); \
   inline hipError_t launchPlain(const void* i, bool b, const float* t, size_t T, size_t D, void* o, size_t n, int e, \
-                                hipStream_t s) { return launchFirFft(i, b, t, T, D, o, n, e, s, FftMix{}); } \
+                                hipStream_t s) { return launchFirFft(i, b, t, T, D, o, n, e, s, FftMix{}, false); } \
   uint32_t kernelPolicy() { return 0; }                                                              \
   bool firI8MfmaEligible(size_t, size_t, const void*) { return false; }                              \
   bool firI8DecMfmaEligible(size_t, size_t, const void*) { return false; }                           \
@@ -270,6 +270,14 @@ int main() {
           hipDeviceSynchronize();
           std::fill(st.begin(), st.end(), 0ull);
           vars[v].stamps(st.data(), st.size());
+          if (const char* dump = getenv("FFT_BENCH_STAMP_DUMP")) {  // raw stamps: <dump>_<variant>_<round>.bin
+            char path[512];
+            snprintf(path, sizeof path, "%s_%s_%d.bin", dump, vars[v].name, rd);
+            if (FILE* f = fopen(path, "wb")) {
+              fwrite(st.data(), sizeof(unsigned long long), st.size(), f);
+              fclose(f);
+            }
+          }
           std::vector<double> clk, dur, start;
           unsigned long long rtMin = ~0ull;
           for (int wv = 0; wv < 256 * 8; ++wv)

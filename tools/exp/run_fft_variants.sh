@@ -8,7 +8,7 @@
 # names another source file (e.g. a saved baseline).
 set -eu
 cd "$(dirname "$0")/../.."
-OUT=tools/exp/_build_fft
+OUT=${OUT:-tools/exp/_build_fft}
 KSRC=cuda-sdr_amd/csrc/kernels/fir_fft.hip
 VARIANTS=${VARIANTS:-"base|
 nofft|-DGSDR_FFT_EXP=1
