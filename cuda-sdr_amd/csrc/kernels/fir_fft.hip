@@ -43,7 +43,6 @@
 
 #include <atomic>
 #include <cmath>
-#include <mutex>
 
 
 namespace gsdr_amd {
@@ -97,11 +96,6 @@ struct Args {
   uint64_t mixStep;     // by exp(j theta(n)), theta(n) = 2 pi (mixPhase0 + n mixStep) / 2^64
   int32_t outAligned;   // `out` is 16-byte aligned (the D = 1 kernel's row-unit stores)
   int32_t complexTaps;  // taps are {re, im} pairs (gsdrFirCC / gsdrFirCCAmDemod), else real
-  // tail balancing (firFftKernel): blocks [poolStart, nBlocks) are handed out one at a time from a
-  // shared counter (pool[0]) to whichever wave is free; pool[1] counts waves that found it empty, and
-  // the last one zeroes both for the slot's next launch. pool == nullptr: static rounds only.
-  unsigned* pool;
-  int64_t poolStart;
 };
 
 // Tap j (real taps: imaginary part 0).
@@ -722,30 +716,14 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
 
   // round r: workgroup g's wave w takes block (r * groups + g) * kWaves + w, so in every round
   // the grid streams one contiguous stretch of the input (DRAM-friendly, like a grid-stride copy)
-  // and a workgroup's waves read adjacent blocks (their overlapping rows are L2 hits). The last
-  // rounds' blocks (from poolStart) go to waves as they become free: under the board's power cap the
-  // waves progress at different rates (in-kernel stamps: wave spans 358-462 us in a 478 us launch),
-  // so a static split leaves the launch waiting for its slowest waves.
+  // and a workgroup's waves read adjacent blocks (their overlapping rows are L2 hits). The two waves
+  // of a SIMD do not progress alike (r04 stamps: waves 0-3 of a workgroup span ~414 us, waves 4-7
+  // ~452 us of a 478 us launch), but evening that out does not pay: handing the workgroup's blocks to
+  // its waves from an LDS counter, or the last rounds to any free wave from a grid-wide counter, made
+  // every span ~the old maximum and the launch 1.5-5 % slower (the SIMD's throughput is the same
+  // whether one or two waves run it at the end).
   const int64_t stride = (int64_t)gridDim.x * kWaves;
-  const int64_t staticEnd = a.pool != nullptr ? a.poolStart : a.nBlocks;
-  auto next = [&](int64_t b) -> int64_t {
-    if (b + stride < staticEnd) return b + stride;
-    if (a.pool == nullptr) return a.nBlocks;
-    unsigned v = 0;
-    if (l == 0) v = __hip_atomic_fetch_add(a.pool, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t nb = a.poolStart + (int64_t)__builtin_amdgcn_readfirstlane((int)__shfl(v, 0));
-    if (nb >= a.nBlocks && l == 0) {
-      const unsigned waves = gridDim.x * kWaves;
-      if (__hip_atomic_fetch_add(a.pool + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == waves - 1) {
-        // every wave has made its last grab: reset the slot for its next launch
-        __hip_atomic_store(a.pool, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.pool + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    return nb;
-  };
-  const int64_t b0 = (int64_t)blockIdx.x * kWaves + w;
-  for (int64_t b = b0 < staticEnd ? b0 : next(b0 - stride); b < a.nBlocks; b = next(b)) {
+  for (int64_t b = (int64_t)blockIdx.x * kWaves + w; b < a.nBlocks; b += stride) {
     Rows<D, IN> R;
     loadRows<D>(a, b, R, L.scratch, l);
     f2 t[8];
@@ -1101,51 +1079,6 @@ int cuCount() {
   return n;
 }
 
-// Tail-balancing pool rounds (firFftKernel): the last GSDR_FFT_POOL_ROUNDS rounds of blocks are handed
-// out dynamically (0: static rounds only).
-#ifndef GSDR_FFT_POOL_ROUNDS
-#define GSDR_FFT_POOL_ROUNDS 0
-#endif
-
-// Per-device counter slots for the pool (2 words each, zeroed once, reset by each launch's last wave).
-// Eager launches take slots round-robin from the first half, stream captures from the second half, so
-// a slot baked into a graph is never handed to an eager launch; a slot is reused only after 1 024
-// later launches of its kind (a graph replayed concurrently on two streams would share its slot).
-constexpr int kPoolSlots = 1024;
-constexpr int kPoolMaxDevices = 64;
-std::mutex gPoolMu;
-unsigned* gPoolDev[kPoolMaxDevices];
-std::atomic<uint32_t> gPoolSeq{0}, gPoolCapSeq{0};
-
-unsigned* poolSlot(hipStream_t stream) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kPoolMaxDevices) return nullptr;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &cs) != hipSuccess) return nullptr;
-  unsigned* base;
-  {
-    std::lock_guard<std::mutex> lock(gPoolMu);
-    if (gPoolDev[dev] == nullptr) {
-      // not a stream operation: allowed while the caller's stream is being captured
-      hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-      (void)hipThreadExchangeStreamCaptureMode(&mode);
-      void* p = nullptr;
-      if (hipMalloc(&p, 2 * kPoolSlots * 2 * sizeof(unsigned)) == hipSuccess) {
-        if (hipMemset(p, 0, 2 * kPoolSlots * 2 * sizeof(unsigned)) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
-          gPoolDev[dev] = static_cast<unsigned*>(p);
-        else
-          (void)hipFree(p);
-      }
-      (void)hipThreadExchangeStreamCaptureMode(&mode);
-    }
-    base = gPoolDev[dev];
-  }
-  if (base == nullptr) return nullptr;
-  const uint32_t k = cs == hipStreamCaptureStatusNone ? gPoolSeq.fetch_add(1) % kPoolSlots
-                                                      : kPoolSlots + gPoolCapSeq.fetch_add(1) % kPoolSlots;
-  return base + 2 * k;
-}
-
 template <int D, int IN, int EPI, bool MIX>
 hipError_t launchD(fftfir::Args a, hipStream_t stream) {
   using namespace fftfir;
@@ -1157,12 +1090,7 @@ hipError_t launchD(fftfir::Args a, hipStream_t stream) {
   const int64_t maxGroups = cuCount();
   int64_t groups = (a.nBlocks + kWaves - 1) / kWaves;
   if (groups > maxGroups) groups = maxGroups;
-  const int64_t stride = groups * kWaves;
-  a.pool = nullptr;
-  if (GSDR_FFT_POOL_ROUNDS > 0 && a.nBlocks > (GSDR_FFT_POOL_ROUNDS + 2) * stride) {
-    a.pool = poolSlot(stream);
-    a.poolStart = a.nBlocks - (int64_t)GSDR_FFT_POOL_ROUNDS * stride;
-  }
+
   hipLaunchKernelGGL(kernel, dim3((unsigned)groups), dim3(kThreads), lds, stream, a);
   return hipGetLastError();
 }

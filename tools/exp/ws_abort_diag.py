@@ -42,9 +42,14 @@ def scenario(spin):
     try:
         c = chain_mod.AmChain(rf, D, au, Da, L)
         out = torch.empty(4 * (L // (D * Da)), dtype=torch.float32, device="cuda")
+        # the test's sequence, within the resident API's contract (a non-first step reads its RF
+        # history in place in front of its input, so it must be a later view of the same stream; after
+        # a failed step the chain is reset and the next step is a first step again)
         for k in range(3):
+            if k == 2:
+                c.reset()  # step 2 starts the stream again at dev[0] (a first step) in every case
             try:
-                c.step_resident(dev[2 * L * (k % 2) * 2:], 2, out)
+                c.step_resident(dev if k != 1 else dev[2 * L * 2:], 2, out)
             except HipError:
                 failed += 1
             c.torch_stream.synchronize()
