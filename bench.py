@@ -31,6 +31,7 @@ second CPU line).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -542,16 +543,24 @@ def timed_steps(chain, steps, warmup, world, backend, device, local, ops):
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     ops.fft_direct_blocks(local, reset=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        chain.step(evs[i])
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    # no Python garbage collection inside the timed region: a C2 step is ~40 us of GPU time, and one
+    # collection pause of the objects the earlier workloads left (~10 ms) inflated a 50-step C2 line
+    # 5x in an r04 default run (0.221 ms/step beside 0.036 ms launches)
+    gc.collect()
+    gc.disable()
+    try:
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            chain.step(evs[i])
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    finally:
+        gc.enable()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -841,7 +850,7 @@ def main():
                       getattr(chain, "n_slots", 1))
         del chain
         torch.cuda.empty_cache()
-        for wl, k, w in (("c4s", 6, 2), ("c5", 20, 3), ("c2", 50, 5)):
+        for wl, k, w in (("c4s", 6, 2), ("c5", 40, 3), ("c2", 400, 5)):
             xc = (AmChainSharded(ops, rank, world, device, stage) if wl == "c5" else
                   ShardedChain(ops, wl, rank, world, device, stage))
             e2, k2, _ = timed_steps(xc, k, w, world, args.backend, device, local, ops)
