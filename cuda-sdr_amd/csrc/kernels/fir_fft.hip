@@ -325,18 +325,24 @@ __device__ __forceinline__ void fftFwd(f2 (&z)[NP][8], const Lds& L, int l) {
   for (int n = 0; n < NP; ++n) dft8<false>(z[n]);  // over a -> d
 }
 
-// Inverse (unscaled) 512-point DFT from layout F: out lane L, z[h] = y[L + 64 h].
-__device__ __forceinline__ void ifft512(f2 (&zz)[1][8], const Lds& L, int l) {
+// Inverse (unscaled) 512-point DFTs of NP columns from layout F: out lane L, z[n][h] = y_n[L + 64 h].
+// NP = 2 issues both columns' exchange writes before their reads, so one column's LDS round trip
+// overlaps the other's (the D = 1 kernel runs one wave per SIMD: nothing else hides it).
+template <int NP = 1>
+__device__ __forceinline__ void ifft512(f2 (&zz)[NP][8], const Lds& L, int l) {
   f2 t[7];
-  loadTw<1>(t, L, 2);  // W512^-((k0 + 8 c) e)
-  dft8<true>(zz[0]);   // over d -> e (lane 8 k0 + c)
-  twiddleAll<1>(zz, t);
-  loadTw<1>(t, L, 3);  // W64^-(k0 g)
-  exchangeB<1>(zz, L.scratch, l);  // -> lane 8 k0 + e, reg c
-  dft8<true>(zz[0]);   // over c -> g
-  twiddleAll<1>(zz, t);
-  exchangeA<1>(zz, L.scratch, l);  // -> lane e + 8 g, reg k0
-  dft8<true>(zz[0]);   // over k0 -> h
+  loadTw<NP>(t, L, 2);  // W512^-((k0 + 8 c) e)
+#pragma unroll
+  for (int n = 0; n < NP; ++n) dft8<true>(zz[n]);  // over d -> e (lane 8 k0 + c)
+  twiddleAll<NP>(zz, t);
+  loadTw<NP>(t, L, 3);  // W64^-(k0 g)
+  exchangeB<NP>(zz, L.scratch, l);  // -> lane 8 k0 + e, reg c
+#pragma unroll
+  for (int n = 0; n < NP; ++n) dft8<true>(zz[n]);  // over c -> g
+  twiddleAll<NP>(zz, t);
+  exchangeA<NP>(zz, L.scratch, l);  // -> lane e + 8 g, reg k0
+#pragma unroll
+  for (int n = 0; n < NP; ++n) dft8<true>(zz[n]);  // over k0 -> h
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t blockRsrc(const void* base, int64_t bytes) {
@@ -699,6 +705,21 @@ __device__ __forceinline__ void convolveBlock(const Args& a, const Rows<D, IN>& 
   }
 }
 
+// Workgroup i runs on XCD i mod 8 (round-robin dispatch). Logical group (i mod 8) n / 8 + i / 8 puts
+// consecutive logical groups - whose blocks share their overlap rows - on one XCD, so the re-read
+// rows meet in that XCD's L2 rather than travelling from the fabric twice.
+#ifndef GSDR_FFT_XCD
+#define GSDR_FFT_XCD 1
+#endif
+__device__ __forceinline__ int xcdGroup(int i, int n) {
+  if (!GSDR_FFT_XCD || (n & 7) != 0) return i;
+  return (i & 7) * (n >> 3) + (i >> 3);
+}
+// The D >= 2 kernel's workgroup order (1: xcdGroup, A/B builds; r02 measured it neutral at C3).
+#ifndef GSDR_FFT_XCD_D
+#define GSDR_FFT_XCD_D 0
+#endif
+
 template <int D, int IN, int EPI, bool MIX = false>
 __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) f2 lds[];
@@ -723,7 +744,8 @@ __global__ void __launch_bounds__(kThreads) firFftKernel(Args a) {
   // every span ~the old maximum and the launch 1.5-5 % slower (the SIMD's throughput is the same
   // whether one or two waves run it at the end).
   const int64_t stride = (int64_t)gridDim.x * kWaves;
-  for (int64_t b = (int64_t)blockIdx.x * kWaves + w; b < a.nBlocks; b += stride) {
+  const int grp = GSDR_FFT_XCD_D ? xcdGroup((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  for (int64_t b = (int64_t)grp * kWaves + w; b < a.nBlocks; b += stride) {
     Rows<D, IN> R;
     loadRows<D>(a, b, R, L.scratch, l);
     f2 t[8];
@@ -823,16 +845,6 @@ __device__ __forceinline__ void drainBlockLoads(const PrefetchCf<D>& P, Rows<D, 
 // m < V = 512 - Q.) Then one inverse 512-point FFT per output phase.
 constexpr int kTwD1 = 7 * 8 * 64;  // alpha^-t, t = 1..7: per-lane float4 pairs like G
 
-// Workgroup i runs on XCD i mod 8 (round-robin dispatch). Logical group (i mod 8) n / 8 + i / 8 puts
-// consecutive logical groups - whose blocks share their overlap rows - on one XCD, so the re-read
-// rows meet in that XCD's L2 rather than travelling from the fabric twice.
-#ifndef GSDR_FFT_XCD
-#define GSDR_FFT_XCD 1
-#endif
-__device__ __forceinline__ int xcdGroup(int i, int n) {
-  if (!GSDR_FFT_XCD || (n & 7) != 0) return i;
-  return (i & 7) * (n >> 3) + (i >> 3);
-}
 
 template <int EPI>
 __device__ void directBlockD1(const Args& a, int64_t b, int l) {
@@ -973,26 +985,41 @@ __device__ __forceinline__ void convolveBlockD1(const Args& a, const Rows<8, kCf
   const int64_t row0 = b * (int64_t)a.V;
   // outputs 8 (row0 + m) + r: row m = l + 64 h of output phase r lands in lane l, register h
   float am[D][8];  // EPI == kAm: the envelopes (the complex results go back into X[r])
+  // Output phases inverse-transformed together. Pairs (their exchanges' LDS round trips overlapped)
+  // measured SLOWER: C4 678 -> 752 us per 2^27 samples (profiles/r04/exp/fft_d1_ifft_pairs_ab.log;
+  // the larger live set costs the one-wave-per-SIMD schedule more than the overlap gains). The wave's
+  // scratch holds two exchange columns, so at most 2.
+#ifndef GSDR_FFT_D1_IFFT_NP
+#define GSDR_FFT_D1_IFFT_NP 1
+#endif
+  constexpr int INP = GSDR_FFT_D1_IFFT_NP;
+  static_assert(INP == 1 || INP == 2, "the wave's scratch holds two exchange columns");
 #pragma unroll
-  for (int r = 0; r < D; ++r) {
-    f2 acc[1][8];
-    if (r > 0) {  // Y_r = alpha^r (alpha^-r Y_r): times the conjugate of the twist row r
-      f2 w[8], u[8];
-      loadRow8(w, twist, r - 1);
+  for (int r0 = 0; r0 < D; r0 += INP) {
+    f2 acc[INP][8];
 #pragma unroll
-      for (int d = 0; d < 8; ++d) u[d] = cmul1(X[r][d], w[d]);
+    for (int n = 0; n < INP; ++n) {
+      const int r = r0 + n;
+      if (r > 0) {  // Y_r = alpha^r (alpha^-r Y_r): times the conjugate of the twist row r
+        f2 w[8], u[8];
+        loadRow8(w, twist, r - 1);
 #pragma unroll
-      for (int d = 0; d < 8; ++d) acc[0][d] = cmulc2(X[r][d], w[d], u[d]);
-    } else {
+        for (int d = 0; d < 8; ++d) u[d] = cmul1(X[r][d], w[d]);
 #pragma unroll
-      for (int d = 0; d < 8; ++d) acc[0][d] = X[0][d];
+        for (int d = 0; d < 8; ++d) acc[n][d] = cmulc2(X[r][d], w[d], u[d]);
+      } else {
+#pragma unroll
+        for (int d = 0; d < 8; ++d) acc[n][d] = X[0][d];
+      }
     }
-    ifft512(acc, L, l);
+    ifft512<INP>(acc, L, l);
 #pragma unroll
-    for (int h = 0; h < 8; ++h) {
-      if (EPI == kAm) am[r][h] = amEnvelope(acc[0][h]);
-      else X[r][h] = acc[0][h];
-    }
+    for (int n = 0; n < INP; ++n)
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        if (EPI == kAm) am[r0 + n][h] = amEnvelope(acc[n][h]);
+        else X[r0 + n][h] = acc[n][h];
+      }
   }
   // row m's eight phases are 8 consecutive outputs: stored as 16-byte units (lanes 32 / 64 bytes
   // apart, the whole row range of a register h in one sweep) - phase-strided 4-byte stores left
