@@ -259,8 +259,66 @@ __device__ __forceinline__ void readRows(f2 (&z)[NP][8], const f2* s, int rowOff
       z[n][2 * c + 1] = f2{v.z, v.w};
     }
 }
+// exchangeA in registers (GSDR_FFT_XA_REG): the same permutation - lane a + 8 b, register c receives
+// lane a + 8 c, register b - as three butterfly stages of an 8 x 8 transpose over lane bits 3, 4, 5:
+// DPP row_ror:8 with bank masks (lane ^ 8, register bit 0), v_permlane16_swap (lane ^ 16, register
+// bit 1), v_permlane32_swap (lane ^ 32, register bit 2); no LDS traffic. The swaps are inline asm
+// (the builtins lost their second result under this compiler); s_nop 1 covers the VALU-write ->
+// v_permlane read hazard.
+#ifndef GSDR_FFT_XA_REG
+#define GSDR_FFT_XA_REG 0
+#endif
+template <int BANKS>
+__device__ __forceinline__ float dppRor8(float old, float src) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, src),
+                                                                0x128, 0xF, BANKS, false));
+}
+__device__ __forceinline__ void permSwap16(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void permSwap32(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+template <int W>
+__device__ __forceinline__ void permSwapC(f2& a, f2& b) {  // both components of two complex registers
+  float ax = a.x, ay = a.y, bx = b.x, by = b.y;
+  if (W == 16) {
+    permSwap16(ax, bx);
+    permSwap16(ay, by);
+  } else {
+    permSwap32(ax, bx);
+    permSwap32(ay, by);
+  }
+  a = f2{ax, ay};
+  b = f2{bx, by};
+}
+template <int NP>
+__device__ __forceinline__ void exchangeAReg(f2 (&z)[NP][8]) {
+#pragma unroll
+  for (int n = 0; n < NP; ++n) {
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) {
+      const f2 p = z[n][r], q = z[n][r + 1];
+      z[n][r] = f2{dppRor8<0xC>(p.x, q.x), dppRor8<0xC>(p.y, q.y)};
+      z[n][r + 1] = f2{dppRor8<0x3>(q.x, p.x), dppRor8<0x3>(q.y, p.y)};
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NP; ++n)
+#pragma unroll
+    for (int r : {0, 1, 4, 5}) permSwapC<16>(z[n][r], z[n][r + 2]);
+#pragma unroll
+  for (int n = 0; n < NP; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) permSwapC<32>(z[n][r], z[n][r + 4]);
+}
+
 template <int NP>
 __device__ __forceinline__ void exchangeA(f2 (&z)[NP][8], f2* s, int l) {
+  if constexpr (GSDR_FFT_XA_REG != 0) {
+    exchangeAReg<NP>(z);
+    return;
+  }
   const int a = l & 7, hi = l >> 3;
 #pragma unroll
   for (int n = 0; n < NP; ++n)
