@@ -659,10 +659,26 @@ def host_fed_c5(device, slots=4, warmup=8, steps=48):
     dt = time.perf_counter() - t0
     chain.close()
     msps = steps * C5_CHUNK / dt / 1e6
+    # the link itself: pinned host -> device copies of one chunk's bytes on a side stream (the
+    # ceiling this line can reach; PCIe Gen5 x16 is ~50 GB/s per direction where it is not shared)
+    hb = torch.empty(2 * C5_CHUNK, dtype=torch.int8, pin_memory=True)
+    db = torch.empty(2 * C5_CHUNK, dtype=torch.int8, device=device)
+    cs = torch.cuda.Stream(device)
+    with torch.cuda.stream(cs):
+        for _ in range(3):
+            db.copy_(hb, non_blocking=True)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(cs)
+        for _ in range(20):
+            db.copy_(hb, non_blocking=True)
+        b.record(cs)
+    b.synchronize()
+    h2d_gbs = 20 * 2 * C5_CHUNK / (a.elapsed_time(b) * 1e-3) / 1e9
+    del hb, db
     return {"workload": f"C5 fed from host memory: {slots} pinned hipHostMalloc slots of {C5_CHUNK} int8 IQ samples, "
                         "H2D on the chain's copy stream overlapped with compute, audio back into pinned slots",
             "value": msps, "unit": "Msamples/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
-            "h2d_gbs": msps * 2e6 / 1e9, "audio_samples": audio,
+            "h2d_gbs": msps * 2e6 / 1e9, "h2d_link_probe_gbs": h2d_gbs, "audio_samples": audio,
             "note": "PCIe-inclusive rate, reported beside value (inputs resident in HBM), never as it"}
 
 

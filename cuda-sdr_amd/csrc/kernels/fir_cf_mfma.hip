@@ -644,6 +644,9 @@ constexpr int kAudioLag = 5;
 constexpr int kAmRingMirror = 256;  // ring[4096 + i] = ring[i] for i < 256: no wrap inside a window
 constexpr int kAudioMaxTaps = 256;  // 8 tap groups of 32 per output slot
 
+#ifndef GSDR_WS_WAITS
+#define GSDR_WS_WAITS 0
+#endif
 struct WsCtl {
   int planesFull[2];
   int planesFree[2];
@@ -683,7 +686,35 @@ __device__ __forceinline__ void wsSignal(int* p, int lane) {
   if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Hand-off wait profile, diagnostic builds only (-DGSDR_WS_WAITS=1; the product build has none): per
+// wave of the first 256 workgroups, the shader cycles spent in each kind of wait (the WsCtl counter
+// waited on) and the wave's whole span after its prologue, to tell which hand-off holds which role.
+// Kinds: 0 planesFull, 1 planesFree, 2 partsFull, 3 partsFree, 4 pstat, 5 tapsRead, 6 amFull,
+// 7 amFree; slot 8 = the wave's span, 9 = its wait count.
+#if GSDR_WS_WAITS
+constexpr int kWaitSlots = 10;
+__device__ unsigned long long gWsWaits[256 * 12 * kWaitSlots];
+__device__ __forceinline__ int wsWaitKind(const WsCtl* c, const int* p) {
+  const int off = (int)(p - reinterpret_cast<const int*>(c));  // WsCtl word index
+  return off < 2 ? 0 : off < 4 ? 1 : off < 6 ? 2 : off < 8 ? 3 : off == 8 ? 4 : off == 9 ? 5 : off == 10 ? 6 : 7;
+}
+// Consumer waves only (global atomics: the producers' counted vmcnt waits must not see extra
+// vector-memory operations, and the LDS has no room for per-wave counters); producers record their
+// span once, after their final vmcnt(0).
+__device__ __forceinline__ void wsWaitAdd(WsCtl*, int slot, unsigned long long v) {
+  const int wg = (int)blockIdx.x, w = (int)(threadIdx.x >> 6);
+  if (wg < 256 && w < kCfWaves && (threadIdx.x & 63) == 0) atomicAdd(&gWsWaits[(wg * 12 + w) * kWaitSlots + slot], v);
+}
+__device__ __forceinline__ void wsSpanStore(unsigned long long v) {
+  const int wg = (int)blockIdx.x, w = (int)(threadIdx.x >> 6);
+  if (wg < 256 && (threadIdx.x & 63) == 0) gWsWaits[(wg * 12 + w) * kWaitSlots + 8] = v;
+}
+#endif
+
 __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
+#if GSDR_WS_WAITS
+  const unsigned long long t0w = __builtin_amdgcn_s_memtime();
+#endif
   for (int it = 0;; ++it) {
     const int v = waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (v >= target) break;
@@ -699,6 +730,10 @@ __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
     __builtin_amdgcn_s_sleep(1);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#if GSDR_WS_WAITS
+  wsWaitAdd(c, wsWaitKind(c, p), __builtin_amdgcn_s_memtime() - t0w);
+  wsWaitAdd(c, 9, 1);
+#endif
 }
 
 // Producer window: G units (8 samples, 64 B) per producer thread, unit g = ptid + 256 j; only the
@@ -1490,6 +1525,9 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
 #pragma unroll
   for (int v = 1; v < kCfWaves + kWsProducers; ++v) hMax = fmaxf(hMax, waveMax[v]);
   const int sh = hMax > 0.0f ? 14 - ilogbf(hMax) : 0;  // max |h 2^sh| in [2^14, 2^15)
+#if GSDR_WS_WAITS
+  const unsigned long long span0 = __builtin_amdgcn_s_memtime();
+#endif
 
   if (wave >= kCfWaves) {
     const int ptid = tid - kCfThreads;
@@ -1519,6 +1557,9 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
     if constexpr (AUD)
       for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile(a8, ring, c, t0, lead, t, ptid, ht);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if GSDR_WS_WAITS
+    wsSpanStore(__builtin_amdgcn_s_memtime() - span0);
+#endif
     return;
   }
   CfFirArgs a{};
@@ -1535,6 +1576,9 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
   a.planeStride = a8.planeStride;
   a.dbp = a8.dbp;
   wsConsumers<KS, EPI, true, AUD>(a, smem, part, c, sh, t0, n, tid, a8.dbp != 0, ring, lead);
+#if GSDR_WS_WAITS
+  wsSpanStore(__builtin_amdgcn_s_memtime() - span0);
+#endif
 }
 
 // ---- host side ------------------------------------------------------------------------------
@@ -2092,6 +2136,21 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
 }
 
 }  // namespace gsdr_amd
+
+#if GSDR_WS_WAITS
+extern "C" __attribute__((visibility("default"))) hipError_t gsdrAmdWsWaits(unsigned long long* out, size_t count,
+                                                                             int reset) {
+  hipError_t e = hipDeviceSynchronize();
+  const size_t n = count < (size_t)256 * 12 * gsdr_amd::kWaitSlots ? count : (size_t)256 * 12 * gsdr_amd::kWaitSlots;
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(gsdr_amd::gWsWaits), n * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    void* p = nullptr;
+    e = hipGetSymbolAddress(&p, HIP_SYMBOL(gsdr_amd::gWsWaits));
+    if (e == hipSuccess) e = hipMemset(p, 0, sizeof(unsigned long long) * 256 * 12 * gsdr_amd::kWaitSlots);
+  }
+  return e;
+}
+#endif
 
 #if GSDR_WS_DIAG
 extern "C" __attribute__((visibility("default"))) hipError_t gsdrAmdWsDiag(unsigned long long* out8, int reset) {
