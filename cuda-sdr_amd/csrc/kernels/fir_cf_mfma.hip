@@ -34,6 +34,7 @@
 #include <atomic>
 #include <cstddef>
 #include <mutex>
+#include <vector>
 
 #include "kcommon.h"
 #include "fir_launch.h"
@@ -2103,19 +2104,26 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
   const int Wl = std::min(a.Wu, (511 * a.D + a.T + 7) / 8);
   if (Wl > 4 * kWsPThreads) return hipErrorNotSupported;
   // the layout search costs ~1 ms of host time: cached per (D, KS) like the other launchers' (an
-  // uncached search per call starved the GPU between eager launches: 0.70 ms per C5 step)
+  // uncached search per call starved the GPU between eager launches: 0.70 ms per C5 step); a small
+  // map, so chains with different RF decimations / tap counts stepped alternately stay cached
   static std::mutex layMu;
-  static int layD = -1, layKS = -1;
-  static CfLayout layCached{};
-  CfLayout lay;
+  static std::vector<std::pair<uint64_t, CfLayout>> layCache;
+  CfLayout lay{};
   {
+    const uint64_t key = ((uint64_t)(uint32_t)a.D << 32) | (uint32_t)a.KS;
     std::lock_guard<std::mutex> lock(layMu);
-    if (layD != a.D || layKS != a.KS) {
-      layCached = cfPlaneLayout(a.D, a.KS, a.Wu, 4);
-      layD = a.D;
-      layKS = a.KS;
+    bool found = false;
+    for (const auto& [k, v] : layCache)
+      if (k == key) {
+        lay = v;
+        found = true;
+        break;
+      }
+    if (!found) {
+      lay = cfPlaneLayout(a.D, a.KS, a.Wu, 4);
+      if (layCache.size() >= 16) layCache.erase(layCache.begin());
+      layCache.emplace_back(key, lay);
     }
-    lay = layCached;
   }
   if (lay.planeStride == 0) return hipErrorNotSupported;
   a.padShift = lay.padShift;

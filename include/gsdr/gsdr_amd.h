@@ -170,7 +170,10 @@ GSDR_API hipError_t gsdrAmdFftDirectBlocks(int32_t device, uint64_t* count, int 
 GSDR_API void gsdrAmdSetWsSpinLimit(int32_t iterations);
 GSDR_API int32_t gsdrAmdGetWsSpinLimit(void);
 GSDR_API hipError_t gsdrAmdWsAborts(int32_t device, uint64_t* count, int reset);
-/* The same count WITHOUT synchronising: Pending peeks (no clear), Take reads and clears. For graph
+/* The count is per DEVICE, not per stream or executor: an abort raised by a launch of another stream
+ * or chain on the same device is reported by whichever wave-specialised call (or executor step)
+ * looks next, and cleared there.
+ * The same count WITHOUT synchronising: Pending peeks (no clear), Take reads and clears. For graph
  * executors: when Pending is nonzero they synchronise their stream, then Take, then fail the step.
  * The eager entry points do the same (device-wide), so a caller that synchronises after a launch
  * gets an abort reported by its next call, and the common case costs no API call. */
