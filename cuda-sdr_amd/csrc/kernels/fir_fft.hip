@@ -528,23 +528,40 @@ struct Rows<D, kI8> {
 
 // Row group j of the block as loaded (16-byte unit 64 i + l of the group in R.v[j][2i..2i+1]) ->
 // rows (R.v[j][p] = x[(l + 64 j) D + p]) through the wave's scratch.
+// Row groups transposed per LDS round trip: two images fit the wave's scratch (2 x 64 RU units =
+// 2 kXch complex at D = 8, 10), so group j + 1's writes are issued before group j's reads and one
+// round trip's latency hides the other's (GSDR_FFT_TPAIR 1). Measured r04: bit-identical and 0.6 %
+// slower on C3, 1 % on C4 (the power cap, not LDS latency, sets the pace), so off.
+#ifndef GSDR_FFT_TPAIR
+#define GSDR_FFT_TPAIR 0
+#endif
 template <int D>
 __device__ __forceinline__ void transposeRows(Rows<D, kCf32>& R, f2* s, int l) {
+  constexpr int H = D / 2, RU = kRowUnits<D>;
+  constexpr int NG = (GSDR_FFT_TPAIR && 2 * 64 * RU * 2 <= 2 * kXch) ? 2 : 1;  // images per round trip
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    f4* s4 = reinterpret_cast<f4*>(s);
-    constexpr int H = D / 2, RU = kRowUnits<D>;
+  for (int j0 = 0; j0 < 8; j0 += NG) {
 #pragma unroll
-    for (int i = 0; i < H; ++i) {  // unit u = 64 i + l of the group: row u / H, unit u % H of it
-      const int u = i * 64 + l;
-      s4[RU == H ? u : (u / H) * RU + u % H] = f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
+    for (int g = 0; g < NG; ++g) {
+      f4* s4 = reinterpret_cast<f4*>(s) + g * 64 * RU;
+      const int j = j0 + g;
+#pragma unroll
+      for (int i = 0; i < H; ++i) {  // unit u = 64 i + l of the group: row u / H, unit u % H of it
+        const int u = i * 64 + l;
+        s4[RU == H ? u : (u / H) * RU + u % H] = f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
+      }
     }
     ldsOrder();
 #pragma unroll
-    for (int p = 0; p < D; p += 2) {  // row l: 16-byte reads (D even), lanes 16 RU bytes apart
-      const f4 u = reinterpret_cast<const f4*>(s)[l * RU + p / 2];
-      R.v[j][p] = f2{u.x, u.y};
-      R.v[j][p + 1] = f2{u.z, u.w};
+    for (int g = 0; g < NG; ++g) {
+      const f4* s4 = reinterpret_cast<const f4*>(s) + g * 64 * RU;
+      const int j = j0 + g;
+#pragma unroll
+      for (int p = 0; p < D; p += 2) {  // row l: 16-byte reads (D even), lanes 16 RU bytes apart
+        const f4 u = s4[l * RU + p / 2];
+        R.v[j][p] = f2{u.x, u.y};
+        R.v[j][p + 1] = f2{u.z, u.w};
+      }
     }
     ldsOrder();
   }
