@@ -648,6 +648,14 @@ constexpr int kAudioMaxTaps = 256;  // 8 tap groups of 32 per output slot
 #ifndef GSDR_WS_WAITS
 #define GSDR_WS_WAITS 0
 #endif
+// hand-off polls: one LDS round trip each (1) or three (0, through r04)
+#ifndef GSDR_WS_POLL
+#define GSDR_WS_POLL 1
+#endif
+// int8 consumers: A-fragment reads in flight ahead of the MFMAs (K-steps)
+#ifndef GSDR_WS_PF
+#define GSDR_WS_PF 3
+#endif
 struct WsCtl {
   int planesFull[2];
   int planesFree[2];
@@ -712,24 +720,50 @@ __device__ __forceinline__ void wsSpanStore(unsigned long long v) {
 }
 #endif
 
+// A hand-off that never completes: release every other wait so the grid drains, and count the
+// failure where the host sees it (the entry points report it as hipErrorLaunchTimeOut). The count
+// goes through the global address space: a FLAT atomic would count on lgkmcnt too and turn every
+// later LDS wait of the wave into a full drain (lgkmcnt(0)).
+__device__ __forceinline__ void wsRaiseAbort(WsCtl* c) {
+  __hip_atomic_store(&c->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if ((threadIdx.x & (kWave - 1)) == 0 && c->abortOut != nullptr)
+    __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t*)(c->abortOut), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
 #if GSDR_WS_WAITS
   const unsigned long long t0w = __builtin_amdgcn_s_memtime();
 #endif
+#if GSDR_WS_POLL
+  // one LDS round trip per poll: the counter and the abort word read together, the spin limit
+  // once (reading the three one after the other, each waited for, made a poll ~3 round trips,
+  // added to the hand-off latency of every wait that polls)
+  if (waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target) {
+    const int lim = waveUniform(c->spinLimit);
+    for (int it = 0;; ++it) {
+      __builtin_amdgcn_s_sleep(1);
+      const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int ab = __hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (waveUniform(v) >= target || waveUniform(ab)) break;
+      if (it > lim) {
+        wsRaiseAbort(c);
+        break;
+      }
+    }
+  }
+#else
   for (int it = 0;; ++it) {
     const int v = waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (v >= target) break;
     if (waveUniform(__hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
     if (it > c->spinLimit) {
-      // a hand-off that never completes: release every other wait so the grid drains, and count
-      // the failure where the host sees it (the entry points report it as hipErrorLaunchTimeOut)
-      __hip_atomic_store(&c->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if ((threadIdx.x & (kWave - 1)) == 0 && c->abortOut != nullptr)
-        __hip_atomic_fetch_add(c->abortOut, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      wsRaiseAbort(c);
       break;
     }
     __builtin_amdgcn_s_sleep(1);
   }
+#endif
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 #if GSDR_WS_WAITS
   wsWaitAdd(c, wsWaitKind(c, p), __builtin_amdgcn_s_memtime() - t0w);
@@ -1003,30 +1037,31 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
     }
     const int8_t* pI = smem + set * NP * a.planeStride + comp * a.planeStride;
     v16f acc = v16f{};
-    // A fragments one K-step ahead; the empty asm keeps the scheduler from hoisting more reads
-    // (168 VGPRs: the tap fragments already hold 88). int8 input: one plane per component (x'
-    // exact in f16), cf32: two limbs.
-    h8 x0, x1 = h8{};
-    {
-      const int off = 16 * cfPhys(uRow + 2 * wave * KS, a.padShift);
-      x0 = *reinterpret_cast<const h8*>(pI + off);
-      if (!I8) x1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
-    }
+    // A fragments PF K-steps ahead; the empty asm keeps the scheduler from hoisting more reads
+    // (the tap fragments already hold 88 VGPRs). int8 input: one plane per component (x' exact in
+    // f16), cf32: two limbs. With one step ahead the compiler reuses the fragment's registers, so
+    // each step's read is issued behind the previous step's two MFMAs and waited for in full
+    // before the next pair: the LDS latency, not the matrix pipe, paced the step.
+    constexpr int PF = I8 ? GSDR_WS_PF : 1;
+    h8 xa[kCfMaxKS], xb[kCfMaxKS];
+    auto readA = [&](int s) {
+      const int off = 16 * cfPhys(uRow + 2 * (wave * KS + s), a.padShift);
+      xa[s] = *reinterpret_cast<const h8*>(pI + off);
+      if (!I8) xb[s] = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
+    };
+#pragma unroll
+    for (int s = 0; s < PF; ++s)
+      if (s < KS) readA(s);
 #pragma unroll
     for (int s = 0; s < kCfMaxKS; ++s) {
       if (s < KS) {
-        h8 n0 = x0, n1 = x1;
-        if (s + 1 < KS) {
-          const int off = 16 * cfPhys(uRow + 2 * (wave * KS + s + 1), a.padShift);
-          n0 = *reinterpret_cast<const h8*>(pI + off);
-          if (!I8) n1 = *reinterpret_cast<const h8*>(pI + 2 * a.planeStride + off);
-        }
+        if (s + PF < KS) readA(s + PF);
         asm volatile("" ::: "memory");
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bh[s], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x0, bl[s], acc, 0, 0, 0);
-        if (!I8) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(x1, bh[s], acc, 0, 0, 0);
-        x0 = n0;
-        x1 = n1;
+        if (PF > 1) __builtin_amdgcn_sched_barrier(0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bl[s], acc, 0, 0, 0);
+        if (!I8) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xb[s], bh[s], acc, 0, 0, 0);
+        if (PF > 1) __builtin_amdgcn_sched_barrier(0);
       }
     }
     wsSignal(&c->planesFree[set], lane);  // this wave's A reads are complete
