@@ -644,6 +644,7 @@ constexpr int kAmRing = 8;
 constexpr int kAudioLag = 5;
 constexpr int kAmRingMirror = 256;  // ring[4096 + i] = ring[i] for i < 256: no wrap inside a window
 constexpr int kAudioMaxTaps = 256;  // 8 tap groups of 32 per output slot
+constexpr int kGWaves = 4;          // two-group kernel: consumer waves per group
 
 #ifndef GSDR_WS_WAITS
 #define GSDR_WS_WAITS 0
@@ -668,6 +669,7 @@ struct WsCtl {
   int abort;
   int mode[2];                        // per plane set: scale exponent sx, or kWsDirect
   float stat[2][2][kWsProducers];     // [tile parity][max, smallest block max][producer wave]
+  int amSlot[kAmRing];                // two-group kernel: consumer waves done with the AM of ring slot s
   // set once by thread 0 (not part of the zeroed hand-off words above)
   int spinLimit;
   uint32_t* abortOut;
@@ -1190,6 +1192,10 @@ struct I8DecArgs {
   int32_t aT;
   int32_t aD;
   int32_t amH;
+  // two-group kernel (firI8WsGroupKernel): B fragments from shifted tap copies in LDS
+  int32_t kneed;     // K-steps of 16 that meet nonzero taps
+  int32_t tcLen;     // f16 elements per tap copy
+  int32_t tcStride;  // bytes between two tap-copy arrays (hi / lo limb of each shift)
 };
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -1399,14 +1405,14 @@ struct NoPre {
   __device__ void operator()() const {}
 };
 
-template <int G, typename Pre = NoPre>
+template <int G, int NC = kCfWaves, typename Pre = NoPre>
 __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
                                                  int i, int ptid, I8WsWindow<G>& wCur, const Pre& pre = Pre{}) {
   const int lane = ptid & (kWave - 1);
   const int set = i & 1;
   pre();
   wsI8WaitWindow<2 * G>(wCur);
-  wsWait(c, &c->planesFree[set], kCfWaves * (i >> 1));
+  wsWait(c, &c->planesFree[set], NC * (i >> 1));
   int8_t* planes = smem + set * 2 * a.planeStride;
   const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
 #pragma unroll
@@ -1440,13 +1446,23 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 constexpr int kAudioTapsPerLane = kAudioMaxTaps / 8;
 
 
+template <bool GRP = false>
 __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* ring, WsCtl* c, int t0, bool lead, int t,
                                             int ptid, const float (&ht)[kAudioTapsPerLane]) {
   const int lane = ptid & (kWave - 1);
   const int pw = ptid >> 6;
   const int o = lane >> 3, q = lane & 7;
   if (!(lead && t == 0)) {
-    wsWait(c, &c->amFull, kCfWaves * (t + 1));
+    if constexpr (GRP) {
+      // tiles finish out of order across the two groups: wait for the ring slots of tiles t and
+      // t - 1 (a window spans at most 256 AM samples); slot s is written by tiles s, s + 8, ...,
+      // each signalled by the 4 waves of its group, and no tile's slot is rewritten before the
+      // audio of the tile after it is done (amFree), so the per-slot counts are exact
+      wsWait(c, &c->amSlot[t & (kAmRing - 1)], kGWaves * (t / kAmRing + 1));
+      if (t >= 1) wsWait(c, &c->amSlot[(t - 1) & (kAmRing - 1)], kGWaves * ((t - 1) / kAmRing + 1));
+    } else {
+      wsWait(c, &c->amFull, kCfWaves * (t + 1));
+    }
 #if GSDR_WS_DIAG
     wsDiag(0, lane == 0 && c->abort != 0);
 #endif
@@ -1617,6 +1633,214 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
 #endif
 }
 
+// ---- two-group int8 kernel (the fused C5 chain; built with -DGSDR_WS_GROUPS=1 only) ----------
+// Measured r04 (profiles/r04/exp/c5_groups/): bit-identical to firI8WsKernel, all chain / fused /
+// shard / abort tests green, but 263 us per C5 launch against 212 us: the B fragments read from LDS
+// add 176 KB of ds_read_b128 traffic per tile, and while both groups issue MFMAs a CU asks its LDS for
+// ~384 B/clk (peak 256) - the latency the groups hide is paid again as LDS bandwidth. Kept for the
+// record, off.
+#ifndef GSDR_WS_GROUPS
+#define GSDR_WS_GROUPS 0
+#endif
+#define GSDR_POLICY_NO_WS_GROUPS 32u  // experimental builds: the 8-way kernel after all
+// firI8WsKernel splits K over all 8 consumer waves: every tile is one round of hand-offs among 8
+// waves for 22 MFMAs per wave, and the per-tile chain of one wave (waits, A reads, MFMAs, partial
+// write / read, epilogue) is latency the matrix pipe sits idle behind (r04: MFMA pipe 34 % busy,
+// LDS 43 %). Here the consumers form two groups of 4 (one wave of each group per SIMD): group g takes
+// the block's tiles i = g, g + 2, ... (plane set g), each wave does TWO of the 8-way K shares (44
+// MFMAs per tile, two accumulators), so a SIMD's two consumer waves work on different tiles and one
+// wave's hand-offs and epilogue overlap the other's MFMAs. The B fragments (taps) come from LDS:
+// 8 / gcd(D, 8) copies of the scaled hi / lo tap limbs, copy r shifted by r elements, so every lane's
+// 8 taps h[kap - col D .. + 7] are one aligned ds_read_b128 (44 fragments per wave would not fit in
+// VGPRs). The 8 partials of a tile are the 8-way kernel's, summed in its order: outputs are bit-
+// identical to firI8WsKernel's.
+template <int KS, bool AUD>
+__device__ __forceinline__ void wsConsumersGroup(const I8DecArgs& a, int8_t* smem, float* part, const int8_t* tc, WsCtl* c,
+                                                 int sh, int t0, int n, int tid, float* ring, bool lead) {
+  constexpr int KW = 2 * KS;  // K-steps per wave
+  constexpr int PF = GSDR_WS_PF;
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int gr = wave >> 2, kq = wave & 3;
+  const int D = a.D, off0 = 31 * D;
+  const int half = lane >> 5, col = lane & 31;
+  const int gd = (D & 1) ? 1 : (D & 2) ? 2 : (D & 4) ? 4 : 8;  // gcd(D, 8)
+  // taps part[p .. p + 7], p = off0 + 16 gs + 8 half - col D, from the copy shifted by r = -p mod 8
+  const int r = (8 - ((off0 - col * D) & 7)) & 7;
+  const int bHi0 = 2 * (r / gd) * a.tcStride + 2 * (off0 - col * D + r + 8 * half);
+  const int bLo0 = bHi0 + a.tcStride;
+  const int kneed = waveUniform(a.kneed);
+  const int arow = lane & 15;
+  const int comp = (lane >> 4) & 1;
+  const int uRow = 4 * D * arow + half;
+  float* pg = part + gr * (kCfPartialBytes / 4);
+  const float outScale = ldexpf(1.0f / 127.0f, -sh);
+  for (int i = gr; i < n; i += 2) {
+    const int set = i & 1;
+    const int gi = i >> 1;  // the group's tile count
+    const int tile = t0 + i;
+    wsWait(c, &c->planesFull[set], kWsProducers * (gi + 1));
+    const int8_t* pI = smem + set * 2 * a.planeStride + comp * a.planeStride;
+    v16f acc0 = v16f{}, acc1 = v16f{};
+    h8 xa[KW], bh[KW], bl[KW];
+    auto readAB = [&](int s) {
+      const int gs = kq * KW + s;
+      xa[s] = *reinterpret_cast<const h8*>(pI + 16 * cfPhys(uRow + 2 * gs, a.padShift));
+      // K-steps past the last nonzero tap read 8 zeros at a copy's start (part index < 8 <= off0)
+      const bool live = gs < kneed;
+      bh[s] = *reinterpret_cast<const h8*>(tc + (live ? bHi0 + 32 * gs : 0));
+      bl[s] = *reinterpret_cast<const h8*>(tc + (live ? bLo0 + 32 * gs : 0));
+    };
+#pragma unroll
+    for (int s = 0; s < PF; ++s)
+      if (s < KW) readAB(s);
+#pragma unroll
+    for (int s = 0; s < KW; ++s) {
+      if (s + PF < KW) readAB(s + PF);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (s < KS) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bh[s], acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bl[s], acc0, 0, 0, 0);
+      } else {
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bh[s], acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bl[s], acc1, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wsSignal(&c->planesFree[set], lane);  // this wave's A reads are complete
+    // partials: accumulator a of wave kq is share v = 2 kq + a of the 8-way kernel
+    wsWait(c, &c->partsFree[gr], kGWaves * gi);  // the group's previous tile reduced
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      pg[((2 * kq) * 16 + k) * kWave + lane] = acc0[k];
+      pg[((2 * kq + 1) * 16 + k) * kWave + lane] = acc1[k];
+    }
+    wsSignal(&c->partsFull[gr], lane);
+    wsWait(c, &c->partsFull[gr], kGWaves * (gi + 1));
+    // wave kq reduces accumulator registers kq, kq + 4 (I) and kq + 8, kq + 12 (Q) in the 8-way
+    // kernel's order (shares 0..7)
+    float yi[2] = {0.0f, 0.0f}, yq[2] = {0.0f, 0.0f};
+#pragma unroll
+    for (int v = 0; v < kCfWaves; ++v)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        yi[h] += pg[(v * 16 + kq + 4 * h) * kWave + lane];
+        yq[h] += pg[(v * 16 + kq + 4 * h + 8) * kWave + lane];
+      }
+    wsSignal(&c->partsFree[gr], lane);
+    if (AUD && i - kAmRing + 2 > 0) wsWait(c, &c->amFree, kWsProducers * (i - kAmRing + 2));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int orow = kq + 8 * h + 4 * half;
+      const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
+      const float v = __builtin_amdgcn_sqrtf(fmaf(yi[h], yi[h], yq[h] * yq[h])) * outScale;
+      if constexpr (AUD) {
+        const int pos = (i & (kAmRing - 1)) * kCfTileOut + 32 * orow + col;
+        const float rv = k < a.nOut ? v : 0.0f;
+        ring[pos] = rv;
+        if (pos < kAmRingMirror) ring[kAmRing * kCfTileOut + pos] = rv;
+        if (a.out != nullptr && k < a.nOut && !(lead && i == 0)) reinterpret_cast<float*>(a.out)[k] = v;
+      } else if (k < a.nOut) {
+        reinterpret_cast<float*>(a.out)[k] = v;
+      }
+    }
+    if constexpr (AUD) wsSignal(&c->amSlot[i & (kAmRing - 1)], lane);
+  }
+}
+
+template <int KS, int G, bool AUD>
+__global__ __launch_bounds__(kWsThreads, 1) void firI8WsGroupKernel(I8DecArgs a8, int Wl) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  float* part = reinterpret_cast<float*>(smem + 4 * a8.planeStride);
+  float* ring = reinterpret_cast<float*>(smem + 4 * a8.planeStride + 2 * kCfPartialBytes);
+  int8_t* tc = smem + 4 * a8.planeStride + 2 * kCfPartialBytes + 4 * (kAmRing * kCfTileOut + kAmRingMirror);
+  __shared__ WsCtl ctl;
+  __shared__ float waveMax[kCfWaves + kWsProducers];
+  WsCtl* c = &ctl;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = waveUniform(tid >> 6);
+  const int D = a8.D, T = a8.T;
+
+  const int q = a8.tiles / (int)gridDim.x, r = a8.tiles % (int)gridDim.x;
+  int t0 = (int)blockIdx.x * q + min((int)blockIdx.x, r);
+  int n = q + ((int)blockIdx.x < r ? 1 : 0);
+  if (n <= 0) return;
+  bool lead = false;  // as firI8WsKernel: the tile before the block's range, for the ring only
+  if (AUD && t0 > 0) {
+    --t0;
+    ++n;
+    lead = true;
+  }
+
+  if (tid < kWsCtlZeroWords) reinterpret_cast<int*>(c)[tid] = 0;
+  if (tid == 0) {
+    c->spinLimit = a8.spinLimit;
+    c->abortOut = a8.abortOut;
+  }
+  const int off0 = 31 * D;
+  float hm = 0.0f;
+  for (int i = tid; i < T; i += kWsThreads) hm = fmaxf(hm, fabsf(a8.taps[i]));
+  for (int i = tid; i < 4 * a8.planeStride / 16; i += kWsThreads) reinterpret_cast<uint4*>(smem)[i] = uint4{0, 0, 0, 0};
+  hm = waveMaxNonNeg(hm);
+  if (lane == 0) waveMax[wave] = hm;
+  __syncthreads();
+  float hMax = waveMax[0];
+#pragma unroll
+  for (int v = 1; v < kCfWaves + kWsProducers; ++v) hMax = fmaxf(hMax, waveMax[v]);
+  const int sh = hMax > 0.0f ? 14 - ilogbf(hMax) : 0;  // max |h 2^sh| in [2^14, 2^15)
+  // tap copies: copy ci (shift ci gd) element j = part[j - ci gd] (part[i] = h[i - off0], zero
+  // outside the taps), scaled by 2^sh and split into f16 hi + lo exactly as the 8-way kernel's
+  // B fragments
+  {
+    const int gd = (D & 1) ? 1 : (D & 2) ? 2 : (D & 4) ? 4 : 8;
+    const int nc = 8 / gd, L = a8.tcLen;
+    for (int e = tid; e < nc * L; e += kWsThreads) {
+      const int ci = e / L, j = e - ci * L;
+      const int ti = j - ci * gd - off0;
+      const float hs = ldexpf((ti >= 0 && ti < T) ? a8.taps[ti] : 0.0f, sh);
+      const _Float16 hi = (_Float16)hs;
+      reinterpret_cast<_Float16*>(tc + 2 * ci * a8.tcStride)[j] = hi;
+      reinterpret_cast<_Float16*>(tc + (2 * ci + 1) * a8.tcStride)[j] = (_Float16)(hs - (float)hi);
+    }
+  }
+  __syncthreads();
+
+  if (wave >= kCfWaves) {
+    const int ptid = tid - kCfThreads;
+    I8WsWindow<G> wA, wB;
+    const i4v r0 = wsI8TileRsrc(a8, t0, true);
+#pragma unroll
+    for (int j = 0; j < G; ++j) wsI8LoadGroup<G>(r0, Wl, ptid, j, wA);
+    const i4v r1 = wsI8TileRsrc(a8, t0 + 1, n > 1);
+#pragma unroll
+    for (int j = 0; j < G; ++j) wsI8LoadGroup<G>(r1, Wl, ptid, j, wB);
+    float ht[kAudioTapsPerLane];
+#pragma unroll
+    for (int u = 0; u < kAudioTapsPerLane; ++u) {
+      const int tp = (lane & 7) + 8 * u;
+      ht[u] = AUD && tp < a8.aT ? a8.aTaps[tp] : 0.0f;
+    }
+    for (int i = 0;; i += 2) {
+      wsI8ProducerTile<G, kGWaves>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
+        if (AUD && i >= kAudioLag) wsAudioTile<true>(a8, ring, c, t0, lead, i - kAudioLag, ptid, ht);
+      });
+      if (i + 1 >= n) break;
+      wsI8ProducerTile<G, kGWaves>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
+        if (AUD && i + 1 >= kAudioLag) wsAudioTile<true>(a8, ring, c, t0, lead, i + 1 - kAudioLag, ptid, ht);
+      });
+      if (i + 2 >= n) break;
+    }
+    if constexpr (AUD)
+      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile<true>(a8, ring, c, t0, lead, t, ptid, ht);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+  wsConsumersGroup<KS, AUD>(a8, smem, part, tc, c, sh, t0, n, tid, ring, lead);
+}
+
 // ---- host side ------------------------------------------------------------------------------
 
 namespace {
@@ -1635,7 +1859,7 @@ struct CfLayout {
 
 // Pick the plane padding and the I/Q plane offset that minimise the A-fragment bank conflicts
 // for this (D, KS), within the LDS budget.
-CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes) {
+CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes, size_t extra = kCfPartialBytes) {
   CfLayout best{4, 0};
   double bestCost = 1e30;
   for (int p = 4; p >= 1; --p) {
@@ -1643,7 +1867,7 @@ CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes) {
     const int base = (16 * units + 255) / 256 * 256;
     for (int qoff = 0; qoff < 16; ++qoff) {
       const int stride = base + 16 * qoff;
-      if (nPlanes * stride + kCfPartialBytes > kCfDynLdsMax) continue;
+      if (nPlanes * (size_t)stride + extra > (size_t)kCfDynLdsMax) continue;
       double cost = 0;
       for (int s = 0; s < kCfWaves * KS; ++s) {
         for (const auto& grp : kB128Groups) {
@@ -1811,6 +2035,76 @@ hipError_t launchI8WsAudioAny(const I8DecArgs& a, int Wl, size_t lds, int grid, 
     default: return launchI8WsAudioKS<11>(a, Wl, lds, grid, stream);
   }
 }
+
+#if GSDR_WS_GROUPS
+template <int KS, int G>
+hipError_t launchI8WsGroupG(const I8DecArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
+  auto kernel = &firI8WsGroupKernel<KS, G, true>;
+  const hipError_t attrErr = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kCfDynLdsMax);
+  if (attrErr != hipSuccess) return attrErr;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWsThreads), lds, stream, a, Wl);
+  return hipGetLastError();
+}
+
+template <int KS>
+hipError_t launchI8WsGroupKS(const I8DecArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
+  switch ((Wl + kWsPThreads - 1) / kWsPThreads) {
+    case 1: return launchI8WsGroupG<KS, 1>(a, Wl, lds, grid, stream);
+    case 2: return launchI8WsGroupG<KS, 2>(a, Wl, lds, grid, stream);
+    case 3: return launchI8WsGroupG<KS, 3>(a, Wl, lds, grid, stream);
+    default: return launchI8WsGroupG<KS, 4>(a, Wl, lds, grid, stream);
+  }
+}
+
+// the two-group kernel is built for the long filters (8 - 11 K-steps per 8-way share)
+constexpr int kGroupMinKS = 8;
+hipError_t launchI8WsGroupAny(const I8DecArgs& a, int Wl, size_t lds, int grid, hipStream_t stream) {
+  switch (a.KS) {
+    case 8: return launchI8WsGroupKS<8>(a, Wl, lds, grid, stream);
+    case 9: return launchI8WsGroupKS<9>(a, Wl, lds, grid, stream);
+    case 10: return launchI8WsGroupKS<10>(a, Wl, lds, grid, stream);
+    default: return launchI8WsGroupKS<11>(a, Wl, lds, grid, stream);
+  }
+}
+
+// Tap-copy stride of the two-group kernel: 2 tcLen bytes + a pad (16-byte steps, within `room`)
+// that minimises the B-fragment ds_read_b128 bank conflicts (every K-step shifts all lanes alike, so
+// one step's pattern is every step's).
+int groupTapStride(int D, int tcLen, size_t room) {
+  const int off0 = 31 * D;
+  const int gd = (D & 1) ? 1 : (D & 2) ? 2 : (D & 4) ? 4 : 8;
+  const int nc = 8 / gd;
+  int best = -1;
+  int bestCost = 1 << 30;
+  for (int pad = 0; pad <= 240; pad += 16) {
+    const int stride = 2 * tcLen + pad;
+    if ((size_t)2 * nc * stride > room) break;
+    int cost = 0;
+    for (const auto& grp : kB128Groups) {
+      int units[16][16];
+      int cnt[16] = {};
+      int worst = 1;
+      for (int li = 0; li < 16; ++li) {
+        const int l = grp[li], col = l & 31, half = l >> 5;
+        const int r = (8 - ((off0 - col * D) & 7)) & 7;
+        const int unit = (2 * (r / gd) * stride + 2 * (off0 - col * D + r + 8 * half)) / 16;
+        const int slot = unit & 15;
+        bool dup = false;
+        for (int k = 0; k < cnt[slot]; ++k) dup |= units[slot][k] == unit;
+        if (!dup) units[slot][cnt[slot]++] = unit;
+        worst = cnt[slot] > worst ? cnt[slot] : worst;
+      }
+      cost += worst;
+    }
+    if (cost < bestCost) {
+      bestCost = cost;
+      best = stride;
+    }
+  }
+  return best;
+}
+#endif
 
 template <int KS>
 hipError_t launchI8WsKS(const I8DecArgs& a, int Wl, size_t lds, int grid, int epi, hipStream_t stream) {
@@ -2143,27 +2437,56 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
   // map, so chains with different RF decimations / tap counts stepped alternately stay cached
   static std::mutex layMu;
   static std::vector<std::pair<uint64_t, CfLayout>> layCache;
-  CfLayout lay{};
-  {
-    const uint64_t key = ((uint64_t)(uint32_t)a.D << 32) | (uint32_t)a.KS;
+  auto cachedLayout = [&](int tag, size_t extra) {
+    const uint64_t key = ((uint64_t)(uint32_t)a.D << 32) | ((uint64_t)(uint32_t)a.KS << 8) | (uint32_t)tag;
     std::lock_guard<std::mutex> lock(layMu);
-    bool found = false;
     for (const auto& [k, v] : layCache)
-      if (k == key) {
-        lay = v;
-        found = true;
-        break;
+      if (k == key) return v;
+    const CfLayout l = cfPlaneLayout(a.D, a.KS, a.Wu, 4, extra);
+    if (layCache.size() >= 16) layCache.erase(layCache.begin());
+    layCache.emplace_back(key, l);
+    return l;
+  };
+  const size_t ringBytes = sizeof(float) * (kAmRing * kCfTileOut + kAmRingMirror);
+#if GSDR_WS_GROUPS
+  // the two-group kernel (bit-identical outputs; GSDR_POLICY_NO_WS_GROUPS keeps the 8-way one)
+  if ((policy & GSDR_POLICY_NO_WS_GROUPS) == 0 && a.KS >= kGroupMinKS) {
+    const int gd = (a.D & 1) ? 1 : (a.D & 2) ? 2 : (a.D & 4) ? 4 : 8;
+    const int nc = 8 / gd;
+    const int tcLen = (31 * a.D + 16 * ksteps + 8 + 7) / 8 * 8;
+    const size_t fixed = 2 * (size_t)kCfPartialBytes + ringBytes;
+    const CfLayout gl = cachedLayout(1, fixed + (size_t)2 * nc * 2 * tcLen);
+    if (gl.planeStride != 0) {
+      const size_t used = 4 * (size_t)gl.planeStride + fixed;
+      const int stride = used < (size_t)kCfDynLdsMax ? groupTapStride(a.D, tcLen, kCfDynLdsMax - used) : -1;
+      if (stride > 0) {
+        I8DecArgs g = a;
+        g.padShift = gl.padShift;
+        g.planeStride = gl.planeStride;
+        g.dbp = 0;
+        g.aTaps = aTaps;
+        g.aOut = aOut;
+        g.amHist = amHist;
+        g.aN = (int64_t)aN;
+        g.aT = (int32_t)aT;
+        g.aD = (int32_t)aD;
+        g.amH = (int32_t)amH;
+        g.kneed = ksteps;
+        g.tcLen = tcLen;
+        g.tcStride = stride;
+        const size_t glds = used + (size_t)2 * nc * stride;
+        const int grid = (int)(tiles < 256 ? tiles : 256);
+        if (hipError_t e = wsPrepare(stream, g.spinLimit, g.abortOut); e != hipSuccess) return e;
+        return launchI8WsGroupAny(g, Wl, glds, grid, stream);
       }
-    if (!found) {
-      lay = cfPlaneLayout(a.D, a.KS, a.Wu, 4);
-      if (layCache.size() >= 16) layCache.erase(layCache.begin());
-      layCache.emplace_back(key, lay);
     }
   }
+#endif
+  const CfLayout lay = cachedLayout(0, kCfPartialBytes);
   if (lay.planeStride == 0) return hipErrorNotSupported;
   a.padShift = lay.padShift;
   a.planeStride = lay.planeStride;
-  const size_t lds = 4 * (size_t)a.planeStride + 2 * kCfPartialBytes + sizeof(float) * (kAmRing * kCfTileOut + kAmRingMirror);
+  const size_t lds = 4 * (size_t)a.planeStride + 2 * kCfPartialBytes + ringBytes;
   if (lds > (size_t)kCfDynLdsMax) return hipErrorNotSupported;
   a.dbp = 1;
   a.aTaps = aTaps;
