@@ -537,18 +537,24 @@ def timed_steps(chain, steps, warmup, world, backend, device, local, ops):
     """A short settle, W untimed warm-up steps, then K steps between barrier + synchronize on both
     sides; the max over ranks of the wall time, and the mean per-step HIP-event time of the timed
     kernel."""
-    settle(chain.step)
-    for _ in range(warmup):
-        chain.step()
-    torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    ops.fft_direct_blocks(local, reset=True)
     # no Python garbage collection inside the timed region: a C2 step is ~40 us of GPU time, and one
     # collection pause of the objects the earlier workloads left (~10 ms) inflated a 50-step C2 line
-    # 5x in an r04 default run (0.221 ms/step beside 0.036 ms launches)
+    # 5x in an r04 default run (0.221 ms/step beside 0.036 ms launches). The collection runs BEFORE
+    # the settle: run between the warm-up and the timed steps it idled the GPU for 45-62 ms, and the
+    # power controller's answer to that idle (a few fast launches, then a clock dip recovering over
+    # ~40 launches: C3 464 -> 725 -> 500 us, C5 183 -> 226 -> 190 us in one trace,
+    # profiles/r04/exp/bench_idle_gap/) landed inside the timed region: C3 0.56-0.59 ms per step
+    # against 0.48-0.49 ms of kernel time in the same run.
+    ops.fft_direct_blocks(local, reset=True)  # first call outside the timed path (symbol lookup)
     gc.collect()
     gc.disable()
     try:
+        settle(chain.step)
+        for _ in range(warmup):
+            chain.step()
+        ops.fft_direct_blocks(local, reset=True)
+        torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
