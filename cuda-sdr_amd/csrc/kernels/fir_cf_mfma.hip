@@ -653,6 +653,11 @@ constexpr int kGWaves = 4;          // two-group kernel: consumer waves per grou
 #ifndef GSDR_WS_POLL
 #define GSDR_WS_POLL 1
 #endif
+// int8 consumers with two partial buffers: tile i - 1's reduction interleaved with tile i's MFMAs
+// (r04: bit-identical and time-neutral, 171.7-172.9 vs 169.2-174.8 us per C5 launch; off)
+#ifndef GSDR_WS_RED_IL
+#define GSDR_WS_RED_IL 0
+#endif
 // int8 consumers: A-fragment reads in flight ahead of the MFMAs (K-steps)
 #ifndef GSDR_WS_PF
 #define GSDR_WS_PF 3
@@ -931,6 +936,10 @@ __device__ __forceinline__ void wsProducerTile(const CfFirArgs& a, int Wl, int8_
 // local tile index (its partials: buffer j & 1 when double-buffered, else the single buffer),
 // waited for until every wave has written them. `mode`: the tile's scale exponent, or kWsDirect
 // (outputs already stored).
+template <int EPI, bool I8, bool AUD>
+__device__ __forceinline__ void wsReduceFinish(const CfFirArgs& a, WsCtl* c, int sh, int tile, int j, int b, int mode,
+                                               int tid, float yi, float yq, float* ring, bool lead);
+
 template <int EPI, bool I8, bool AUD = false>
 __device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* part, WsCtl* c, int sh, int tile, int j,
                                              bool dbp, int mode, int tid, float* ring = nullptr, bool lead = false) {
@@ -946,6 +955,20 @@ __device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* pa
       yi += pb[(v * 16 + wave) * kWave + lane];
       yq += pb[(v * 16 + wave + 8) * kWave + lane];
     }
+    wsReduceFinish<EPI, I8, AUD>(a, c, sh, tile, j, b, mode, tid, yi, yq, ring, lead);
+  } else {
+    wsSignal(&c->partsFree[b], lane);
+  }
+}
+
+// The rest of a tile's reduction once its sums are formed: release the partial buffer, then the
+// epilogue (AM ring + audio hand-off, or the output store).
+template <int EPI, bool I8, bool AUD>
+__device__ __forceinline__ void wsReduceFinish(const CfFirArgs& a, WsCtl* c, int sh, int tile, int j, int b, int mode,
+                                               int tid, float yi, float yq, float* ring, bool lead) {
+  const int lane = tid & (kWave - 1);
+  const int wave = tid >> 6;
+  {
     wsSignal(&c->partsFree[b], lane);
     const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * (lane >> 5);
     const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + (lane & 31);
@@ -974,8 +997,6 @@ __device__ __forceinline__ void wsReduceTile(const CfFirArgs& a, const float* pa
         else reinterpret_cast<f2*>(a.out)[k] = f2{yi, yq} * outScale;
       }
     }
-  } else {
-    wsSignal(&c->partsFree[b], lane);
   }
 }
 
@@ -1039,6 +1060,20 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
     }
     const int8_t* pI = smem + set * NP * a.planeStride + comp * a.planeStride;
     v16f acc = v16f{};
+    // int8, two partial buffers: tile i - 1's sums are formed between this tile's MFMAs (the wave
+    // would otherwise sit at each dependent MFMA's issue), in the same order as wsReduceTile
+    constexpr bool IL = I8 && GSDR_WS_RED_IL;
+    const bool red = IL && dbp && i >= 1;
+    if (red) wsWait(c, &c->partsFull[(i - 1) & 1], kCfWaves * (((i - 1) >> 1) + 1));
+    // (the reads are unconditional - no branch in the K loop; without a second buffer they stay in
+    // the first, and their values are used only when `red`)
+    const float* pr = part + (dbp ? ((i - 1) & 1) * (kCfPartialBytes / 4) : 0);
+    float ri[kCfWaves], rq[kCfWaves];
+    float yi = 0.0f, yq = 0.0f;
+    auto readP = [&](int v) {
+      ri[v] = pr[(v * 16 + wave) * kWave + lane];
+      rq[v] = pr[(v * 16 + wave + 8) * kWave + lane];
+    };
     // A fragments PF K-steps ahead; the empty asm keeps the scheduler from hoisting more reads
     // (the tap fragments already hold 88 VGPRs). int8 input: one plane per component (x' exact in
     // f16), cf32: two limbs. With one step ahead the compiler reuses the fragment's registers, so
@@ -1058,12 +1093,27 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
     for (int s = 0; s < kCfMaxKS; ++s) {
       if (s < KS) {
         if (s + PF < KS) readA(s + PF);
+        if (IL && s < kCfWaves) readP(s);
         asm volatile("" ::: "memory");
         if (PF > 1) __builtin_amdgcn_sched_barrier(0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bh[s], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bl[s], acc, 0, 0, 0);
         if (!I8) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xb[s], bh[s], acc, 0, 0, 0);
         if (PF > 1) __builtin_amdgcn_sched_barrier(0);
+        if (IL && s >= 1 && s - 1 < kCfWaves) {
+          yi += ri[s - 1];
+          yq += rq[s - 1];
+        }
+      }
+    }
+    if (IL) {  // shares the K loop did not reach (KS < 9)
+#pragma unroll
+      for (int v = 0; v < kCfWaves; ++v) {
+        if (v >= KS) readP(v);
+        if (v >= KS - 1) {
+          yi += ri[v];
+          yq += rq[v];
+        }
       }
     }
     wsSignal(&c->planesFree[set], lane);  // this wave's A reads are complete
@@ -1075,10 +1125,11 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
       wsWait(c, &c->partsFree[b], kCfWaves * (i >> 1));  // tile i - 2 reduced by every wave
       if (i < 2) wsWait(c, &c->tapsRead, kCfWaves);
       float* pb = part + b * (kCfPartialBytes / 4);
+      if (red) wsReduceFinish<EPI, I8, AUD>(a, c, sh, tile - 1, i - 1, (i - 1) & 1, prevMode, tid, yi, yq, ring, lead);
 #pragma unroll
       for (int k = 0; k < 16; ++k) pb[(wave * 16 + k) * kWave + lane] = acc[k];
       wsSignal(&c->partsFull[b], lane);
-      if (i >= 1) wsReduceTile<EPI, I8, AUD>(a, part, c, sh, tile - 1, i - 1, true, prevMode, tid, ring, lead);
+      if (!IL && i >= 1) wsReduceTile<EPI, I8, AUD>(a, part, c, sh, tile - 1, i - 1, true, prevMode, tid, ring, lead);
     } else {
       wsWait(c, &c->partsFree[0], kCfWaves * i);  // every wave has read tile i - 1's partials
       if (i == 0) wsWait(c, &c->tapsRead, kCfWaves);
