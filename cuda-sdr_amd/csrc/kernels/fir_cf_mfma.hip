@@ -669,12 +669,12 @@ struct WsCtl {
   int partsFree[2];
   int pstat;
   int tapsRead;                       // consumer waves done reading the taps staged in `part`
-  int amFull;                         // fused audio stage: consumer waves' AM of a tile in the ring
+  int amFull;                         // (unused since r04: per-slot counts, amSlot)
   int amFree;                         // producer waves done with the audio outputs of a tile
   int abort;
   int mode[2];                        // per plane set: scale exponent sx, or kWsDirect
   float stat[2][2][kWsProducers];     // [tile parity][max, smallest block max][producer wave]
-  int amSlot[kAmRing];                // two-group kernel: consumer waves done with the AM of ring slot s
+  int amSlot[kAmRing];                // fused audio stage: consumer waves' AM signals per ring slot
   // set once by thread 0 (not part of the zeroed hand-off words above)
   int spinLimit;
   uint32_t* abortOut;
@@ -983,7 +983,7 @@ __device__ __forceinline__ void wsReduceFinish(const CfFirArgs& a, WsCtl* c, int
       const float rv = k < a.nOut ? v : 0.0f;
       ring[pos] = rv;
       if (pos < kAmRingMirror) ring[kAmRing * kCfTileOut + pos] = rv;
-      wsSignal(&c->amFull, lane);
+      wsSignal(&c->amSlot[j & (kAmRing - 1)], lane);
       // the lead tile belongs to the previous block (computed here only for the audio windows)
       if (a.out != nullptr && k < a.nOut && !(lead && j == 0)) reinterpret_cast<float*>(a.out)[k] = v;
     } else if (k < a.nOut) {
@@ -1497,23 +1497,25 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 constexpr int kAudioTapsPerLane = kAudioMaxTaps / 8;
 
 
-template <bool GRP = false>
+template <int NSIG = kCfWaves>
 __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* ring, WsCtl* c, int t0, bool lead, int t,
                                             int ptid, const float (&ht)[kAudioTapsPerLane]) {
   const int lane = ptid & (kWave - 1);
   const int pw = ptid >> 6;
   const int o = lane >> 3, q = lane & 7;
   if (!(lead && t == 0)) {
-    if constexpr (GRP) {
-      // tiles finish out of order across the two groups: wait for the ring slots of tiles t and
-      // t - 1 (a window spans at most 256 AM samples); slot s is written by tiles s, s + 8, ...,
-      // each signalled by the 4 waves of its group, and no tile's slot is rewritten before the
-      // audio of the tile after it is done (amFree), so the per-slot counts are exact
-      wsWait(c, &c->amSlot[t & (kAmRing - 1)], kGWaves * (t / kAmRing + 1));
-      if (t >= 1) wsWait(c, &c->amSlot[(t - 1) & (kAmRing - 1)], kGWaves * ((t - 1) / kAmRing + 1));
-    } else {
-      wsWait(c, &c->amFull, kCfWaves * (t + 1));
-    }
+    // the ring slots of tiles t and t - 1 (a window spans at most 256 AM samples). Slot s holds
+    // tiles s, s + 8, ..., each signalled by the NSIG consumer waves that write it, and no slot is
+    // rewritten before the audio of the tile after its occupant is done (amFree), so a slot's count
+    // says exactly which of its tiles are complete. (A single tile counter, waited for at
+    // NSIG (t + 1), was not: a wave that reduced tile t + 1 could signal it before a slower wave
+    // had written its part of tile t - the count was reached with tile t incomplete. With short
+    // filters - 2 K-steps per wave, little MFMA work between the hand-offs - that happened: r04,
+    // test_am_chain_device_steps at T = 127 / D = 1 and T = 64 / D = 3.)
+    // Tile t - 1's slot was waited for by this wave's previous call (audio tiles run in order),
+    // except when that call was the lead tile's, which has no outputs and waits for nothing.
+    wsWait(c, &c->amSlot[t & (kAmRing - 1)], NSIG * (t / kAmRing + 1));
+    if (lead && t == 1) wsWait(c, &c->amSlot[0], NSIG);
 #if GSDR_WS_DIAG
     wsDiag(0, lane == 0 && c->abort != 0);
 #endif
@@ -1876,16 +1878,16 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsGroupKernel(I8DecArgs a8
     }
     for (int i = 0;; i += 2) {
       wsI8ProducerTile<G, kGWaves>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
-        if (AUD && i >= kAudioLag) wsAudioTile<true>(a8, ring, c, t0, lead, i - kAudioLag, ptid, ht);
+        if (AUD && i >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, lead, i - kAudioLag, ptid, ht);
       });
       if (i + 1 >= n) break;
       wsI8ProducerTile<G, kGWaves>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
-        if (AUD && i + 1 >= kAudioLag) wsAudioTile<true>(a8, ring, c, t0, lead, i + 1 - kAudioLag, ptid, ht);
+        if (AUD && i + 1 >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, lead, i + 1 - kAudioLag, ptid, ht);
       });
       if (i + 2 >= n) break;
     }
     if constexpr (AUD)
-      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile<true>(a8, ring, c, t0, lead, t, ptid, ht);
+      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile<kGWaves>(a8, ring, c, t0, lead, t, ptid, ht);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }

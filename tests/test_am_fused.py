@@ -124,3 +124,17 @@ def test_fused_chain_rejects_short_am(ops, orc):
     r = lib().gsdrInt8FirFCAmDemodFirFF(10, rf.data_ptr(), 1023, iq.data_ptr(), 1000, win.data_ptr(), 0, 1, 20,
                                         au.data_ptr(), 255, out.data_ptr(), 100, 0, None)
     assert r != 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,D,Ta,Da", [(127, 1, 63, 4), (64, 3, 31, 5)])
+def test_fused_chain_short_filters_ring_order(ops, orc, T, D, Ta, Da):
+    """Short RF filters (2 K-steps per consumer wave): the consumer waves hand tiles off quickly, and
+    a wave could finish tile t + 1 before a slower one had written its share of tile t. The audio
+    stage must wait for each ring tile it reads (per-slot counts), not for a tile count; r04 caught
+    the old single counter at these shapes (test_am_chain_device_steps). Repeated launches over
+    random data, every one against the float64 oracle (AM not stored: at D = 1 the plain call runs
+    another kernel, so the AM samples are not the bit-equality reference here)."""
+    for rep in range(12):
+        _run(ops, orc, T, D, Ta, Da, 0, 25_000 + 509 * rep, 0, seed=1000 * T + rep, store=False,
+             check_kernel=False)
