@@ -518,17 +518,36 @@ def spawn_ranks(n, share_gpu=False):
 SETTLE_S = 0.25  # untimed settle before the warm-up steps (see settle)
 
 
-def settle(step, seconds=SETTLE_S):
+def settle(step, seconds=SETTLE_S, world=1, device=None, backend="nccl"):
     """Run `step` untimed for ~`seconds`: after idle the GPU needs ~10-20 ms of load to leave its
     low-clock power state - the first ~20-30 C3 launches take 0.66 ms instead of 0.48 ms
     (profiles/r03/exp/c3_bench_loop_probe.log) - so 5 warm-up steps alone left the timed steps in
-    the ramp. Nothing timed is skipped: the K timed steps still do the full work."""
+    the ramp. Nothing timed is skipped: the K timed steps still do the full work.
+    With several ranks every rank must run the SAME number of steps (each step exchanges halos
+    with the ring neighbours; a rank one step short leaves its neighbour waiting for a halo that
+    never comes - a 2-rank C5 run hung that way in r04): rank 0 times 8 steps, picks the count for
+    `seconds` and broadcasts it."""
+    if world == 1:
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < seconds and n < 4096:
+            step()
+            n += 1
+            if n % 8 == 0:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        return
     t0 = time.perf_counter()
-    n = 0
-    while time.perf_counter() - t0 < seconds and n < 4096:
+    for _ in range(8):
         step()
-        n += 1
-        if n % 8 == 0:
+    torch.cuda.synchronize()
+    per = max((time.perf_counter() - t0) / 8, 1e-6)
+    more = torch.tensor([max(0, min(4096, int(seconds / per)) - 8)], dtype=torch.int64,
+                        device=device if backend == "nccl" else "cpu")
+    dist.broadcast(more, 0)
+    for i in range(int(more.item())):
+        step()
+        if (i + 1) % 8 == 0:
             torch.cuda.synchronize()
     torch.cuda.synchronize()
 
@@ -550,7 +569,11 @@ def timed_steps(chain, steps, warmup, world, backend, device, local, ops):
     gc.collect()
     gc.disable()
     try:
-        settle(chain.step)
+        if world > 1:
+            # ranks start the settle together, so they also leave it together: a rank that waited
+            # long at the barrier before the timed steps would start them after an idle gap
+            dist.barrier()
+        settle(chain.step, world=world, device=device, backend=backend)
         for _ in range(warmup):
             chain.step()
         ops.fft_direct_blocks(local, reset=True)

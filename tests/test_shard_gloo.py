@@ -139,3 +139,43 @@ def test_halo_byte_views():
     assert _bytes(i8[4:]).numel() == 16
     with pytest.raises(ValueError):
         _bytes(torch.zeros(4, 4, dtype=torch.complex64)[:, 1])
+
+
+def _settle_rank(rank, world, port, out_dir):
+    import sys
+    import time
+    sys.path[:0] = [REPO, os.path.join(REPO, "cuda-sdr_amd")]
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize = lambda *a, **k: None  # CPU run: the bench's stream syncs are no-ops here
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    count = [0]
+    buf = torch.zeros(4)
+
+    def step():  # a ring exchange per step, like the sharded chains; ranks run at different speeds
+        time.sleep(0.002 * (1 + rank))
+        nxt, prv = (rank + 1) % world, (rank - 1) % world
+        reqs = [dist.isend(buf.clone(), nxt), dist.irecv(torch.empty(4), prv)]
+        for r in reqs:
+            r.wait()
+        count[0] += 1
+
+    bench.settle(step, seconds=0.08, world=world, backend="gloo")
+    np.save(os.path.join(out_dir, f"settle{rank}.npy"), np.array([count[0]]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_settle_same_step_count_on_every_rank(tmp_path, world):
+    """bench.settle at N > 1 runs the same number of steps on every rank (each step exchanges halos;
+    a rank one step short would leave its neighbour waiting for a halo - a 2-rank C5 bench hung that
+    way in r04 when the settle was timed per rank)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_settle_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    counts = [int(np.load(os.path.join(tmp_path, f"settle{r}.npy"))[0]) for r in range(world)]
+    assert len(set(counts)) == 1 and counts[0] >= 8, counts
