@@ -653,6 +653,10 @@ constexpr int kGWaves = 4;          // two-group kernel: consumer waves per grou
 #ifndef GSDR_WS_POLL
 #define GSDR_WS_POLL 1
 #endif
+// s_sleep argument between hand-off polls (units of 64 clocks; 0: spin on the LDS read alone)
+#ifndef GSDR_WS_SLEEP
+#define GSDR_WS_SLEEP 1
+#endif
 // int8 consumers with two partial buffers: tile i - 1's reduction interleaved with tile i's MFMAs
 // (r04: bit-identical and time-neutral, 171.7-172.9 vs 169.2-174.8 us per C5 launch; off)
 #ifndef GSDR_WS_RED_IL
@@ -749,7 +753,7 @@ __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
   if (waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target) {
     const int lim = waveUniform(c->spinLimit);
     for (int it = 0;; ++it) {
-      __builtin_amdgcn_s_sleep(1);
+      if (GSDR_WS_SLEEP > 0) __builtin_amdgcn_s_sleep(GSDR_WS_SLEEP);
       const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const int ab = __hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (waveUniform(v) >= target || waveUniform(ab)) break;
