@@ -1627,6 +1627,13 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
     hm = fmaxf(hm, fabsf(h));
   }
   for (int i = tid; i < 4 * a8.planeStride / 16; i += kWsThreads) reinterpret_cast<uint4*>(smem)[i] = uint4{0, 0, 0, 0};
+  // the AM ring starts zeroed: an audio window reads 256 ring samples whatever the tap count, the
+  // ones past its taps multiplied by zero - and 0 * NaN is NaN, so a slot this block never writes
+  // (its tiles fill fewer than 8) must not hold whatever the LDS held before the launch (r04: NaN
+  // audio outputs in short-filter steps on fresh boxes, 2 of 6 full-suite runs)
+  if constexpr (AUD)
+    for (int i = tid; i < (kAmRing * kCfTileOut + kAmRingMirror) / 4; i += kWsThreads)
+      reinterpret_cast<uint4*>(ring)[i] = uint4{0, 0, 0, 0};
   hm = waveMaxNonNeg(hm);
   if (lane == 0) waveMax[wave] = hm;
   __syncthreads();
@@ -1841,6 +1848,13 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsGroupKernel(I8DecArgs a8
   float hm = 0.0f;
   for (int i = tid; i < T; i += kWsThreads) hm = fmaxf(hm, fabsf(a8.taps[i]));
   for (int i = tid; i < 4 * a8.planeStride / 16; i += kWsThreads) reinterpret_cast<uint4*>(smem)[i] = uint4{0, 0, 0, 0};
+  // the AM ring starts zeroed: an audio window reads 256 ring samples whatever the tap count, the
+  // ones past its taps multiplied by zero - and 0 * NaN is NaN, so a slot this block never writes
+  // (its tiles fill fewer than 8) must not hold whatever the LDS held before the launch (r04: NaN
+  // audio outputs in short-filter steps on fresh boxes, 2 of 6 full-suite runs)
+  if constexpr (AUD)
+    for (int i = tid; i < (kAmRing * kCfTileOut + kAmRingMirror) / 4; i += kWsThreads)
+      reinterpret_cast<uint4*>(ring)[i] = uint4{0, 0, 0, 0};
   hm = waveMaxNonNeg(hm);
   if (lane == 0) waveMax[wave] = hm;
   __syncthreads();
