@@ -130,11 +130,11 @@ def test_fused_chain_rejects_short_am(ops, orc):
 @pytest.mark.parametrize("T,D,Ta,Da", [(127, 1, 63, 4), (64, 3, 31, 5)])
 def test_fused_chain_short_filters_ring_order(ops, orc, T, D, Ta, Da):
     """Short RF filters (2 K-steps per consumer wave): the consumer waves hand tiles off quickly, and
-    a wave could finish tile t + 1 before a slower one had written its share of tile t. The audio
-    stage must wait for each ring tile it reads (per-slot counts), not for a tile count; r04 caught
-    the old single counter at these shapes (test_am_chain_device_steps). Repeated launches over
-    random data, every one against the float64 oracle (AM not stored: at D = 1 the plain call runs
-    another kernel, so the AM samples are not the bit-equality reference here)."""
+    a wave could finish tile t + 1 before a slower one had written its share of tile t - the audio
+    stage waits for each ring slot it reads (per-slot counts), not for a tile count. Repeated
+    launches of varying tile counts over random data, every one against the float64 oracle (AM not
+    stored: at D = 1 the plain call runs another kernel, so the AM samples are not the bit-equality
+    reference here)."""
     for rep in range(12):
         _run(ops, orc, T, D, Ta, Da, 0, 25_000 + 509 * rep, 0, seed=1000 * T + rep, store=False,
              check_kernel=False)
