@@ -192,7 +192,28 @@ __global__ __launch_bounds__(kBlock) void hbmProbeKernel(const f4* __restrict__ 
   if (MODE == 0 && acc == -1.2345e-38f) out[0] = f4{acc, acc, acc, acc};
 }
 
+// ---- LDS poison (tests): fill every CU's LDS with a pattern so a kernel that reads LDS it never
+// wrote shows it (a NaN pattern turns 0 * stale into NaN) ------------------------------------------
+constexpr int kPoisonLdsBytes = 160 * 1024 - 256;
+__global__ __launch_bounds__(1024) void ldsPoisonKernel(uint32_t pattern) {
+  extern __shared__ uint32_t poisonLds[];
+  for (int i = threadIdx.x; i < kPoisonLdsBytes / 4; i += 1024) poisonLds[i] = pattern;
+  __syncthreads();
+}
+
 extern "C" {
+
+hipError_t gsdrAmdPoisonLds(uint32_t pattern, int32_t device, hipStream_t stream) {
+  DevicePush push(device);
+  if (!push.ok) return hipErrorInvalidDevice;
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ldsPoisonKernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kPoisonLdsBytes);
+  if (e != hipSuccess) return e;
+  int n = 256;
+  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device);
+  hipLaunchKernelGGL(ldsPoisonKernel, dim3((unsigned)(4 * n)), dim3(1024), kPoisonLdsBytes, stream, pattern);
+  return hipGetLastError();
+}
 
 hipError_t gsdrAmdHbmProbe(const void* input, void* output, size_t bytes, int32_t mode, int32_t device,
                            hipStream_t stream) {

@@ -653,6 +653,10 @@ constexpr int kGWaves = 4;          // two-group kernel: consumer waves per grou
 #ifndef GSDR_WS_POLL
 #define GSDR_WS_POLL 1
 #endif
+// fused audio stage: zero the AM ring per launch (0: the r04 defect, for its regression test only)
+#ifndef GSDR_WS_RING_ZERO
+#define GSDR_WS_RING_ZERO 1
+#endif
 // s_sleep argument between hand-off polls (units of 64 clocks; 0: spin on the LDS read alone)
 #ifndef GSDR_WS_SLEEP
 #define GSDR_WS_SLEEP 1
@@ -1631,7 +1635,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
   // ones past its taps multiplied by zero - and 0 * NaN is NaN, so a slot this block never writes
   // (its tiles fill fewer than 8) must not hold whatever the LDS held before the launch (r04: NaN
   // audio outputs in short-filter steps on fresh boxes, 2 of 6 full-suite runs)
-  if constexpr (AUD)
+  if constexpr (AUD && GSDR_WS_RING_ZERO)
     for (int i = tid; i < (kAmRing * kCfTileOut + kAmRingMirror) / 4; i += kWsThreads)
       reinterpret_cast<uint4*>(ring)[i] = uint4{0, 0, 0, 0};
   hm = waveMaxNonNeg(hm);
@@ -1852,7 +1856,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsGroupKernel(I8DecArgs a8
   // ones past its taps multiplied by zero - and 0 * NaN is NaN, so a slot this block never writes
   // (its tiles fill fewer than 8) must not hold whatever the LDS held before the launch (r04: NaN
   // audio outputs in short-filter steps on fresh boxes, 2 of 6 full-suite runs)
-  if constexpr (AUD)
+  if constexpr (AUD && GSDR_WS_RING_ZERO)
     for (int i = tid; i < (kAmRing * kCfTileOut + kAmRingMirror) / 4; i += kWsThreads)
       reinterpret_cast<uint4*>(ring)[i] = uint4{0, 0, 0, 0};
   hm = waveMaxNonNeg(hm);

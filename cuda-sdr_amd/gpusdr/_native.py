@@ -73,6 +73,8 @@ def _declare(L):
     L.gsdrSynthWidebandCf32.restype = err
     L.gsdrAmdHbmProbe.argtypes = [vp, vp, sz, i32, i32, vp]
     L.gsdrAmdHbmProbe.restype = err
+    L.gsdrAmdPoisonLds.argtypes = [ctypes.c_uint32, i32, vp]
+    L.gsdrAmdPoisonLds.restype = err
     L.gsdrAmdBuildId.argtypes = []
     L.gsdrAmdBuildId.restype = ctypes.c_char_p
 

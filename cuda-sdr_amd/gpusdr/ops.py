@@ -185,6 +185,12 @@ def am_chain_fused(taps: torch.Tensor, iq: torch.Tensor, decimation: int, rf_cou
     return audio_out
 
 
+def poison_lds(device: int = 0, pattern: int = 0x7FC00000) -> None:
+    """gsdrAmdPoisonLds on the current stream (tests: stale-LDS reads become visible)."""
+    check(lib().gsdrAmdPoisonLds(pattern, device, ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)),
+          "gsdrAmdPoisonLds")
+
+
 def hbm_probe(src: torch.Tensor, dst: torch.Tensor, mode: int) -> None:
     """gsdrAmdHbmProbe: mode 0 streams src (read bandwidth), mode 1 copies src -> dst."""
     if not (src.is_cuda and dst.is_cuda and src.is_contiguous() and dst.is_contiguous()):

@@ -188,6 +188,9 @@ GSDR_API const char* gsdrAmdBuildId(void);
  * `output`. The bench times it to report the roofline against measured bandwidth as well as spec. */
 GSDR_API hipError_t gsdrAmdHbmProbe(const void* input, void* output, size_t bytes, int32_t mode, int32_t device,
                                     hipStream_t stream);
+/* Tests: fill the LDS of every CU of `device` with the 32-bit `pattern` (one workgroup of the whole
+ * LDS per slot, 4 per CU) on `stream`, so that a later kernel reading LDS it never wrote sees it. */
+GSDR_API hipError_t gsdrAmdPoisonLds(uint32_t pattern, int32_t device, hipStream_t stream);
 
 GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
                                     uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,

@@ -26,7 +26,7 @@ def _expected_audio(orc, am64, rf_bound, audio_taps, Da, n):
     return audio, carried + FIR_TOL * audio_bound + 1e-30
 
 
-def _run(ops, orc, T, D, Ta, Da, n_hist_rf, n_rf, H, seed, store=True, check_kernel=True):
+def _run(ops, orc, T, D, Ta, Da, n_hist_rf, n_rf, H, seed, store=True, check_kernel=True, poison=False):
     """RF outputs [0, n_hist_rf) by the plain call (the history), then the fused call over RF outputs
     [n_hist_rf, n_hist_rf + n_rf) with the last H of the earlier AM samples as its history."""
     import torch
@@ -45,6 +45,8 @@ def _run(ops, orc, T, D, Ta, Da, n_hist_rf, n_rf, H, seed, store=True, check_ker
     window = am_all[n_hist_rf - H:]
     n_audio = (H + n_rf - Ta) // Da + 1
     audio = torch.full((n_audio,), float("nan"), dtype=torch.float32, device="cuda")
+    if poison:  # every CU's LDS filled with NaN just before the launch
+        ops.poison_lds(0)
     ops.am_chain_fused(rf_d, dev[2 * n_hist_rf * D:], D, n_rf, window, H, au_d, Da, n_audio, audio, store_am=store)
     # the two reference calls over the same input
     am_ref = torch.empty(n_rf, dtype=torch.float32, device="cuda")
@@ -138,3 +140,16 @@ def test_fused_chain_short_filters_ring_order(ops, orc, T, D, Ta, Da):
     for rep in range(12):
         _run(ops, orc, T, D, Ta, Da, 0, 25_000 + 509 * rep, 0, seed=1000 * T + rep, store=False,
              check_kernel=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,D,Ta,Da,n_rf", [(64, 3, 31, 5, 1000), (127, 1, 63, 4, 1500), (1023, 10, 255, 20, 1000),
+                                            (1023, 10, 255, 20, 300_000)])
+def test_fused_chain_ignores_stale_lds(ops, orc, T, D, Ta, Da, n_rf):
+    """LDS poisoned with NaN right before each launch: nothing the kernel did not write may reach an
+    output. The audio windows read 256 AM-ring samples and multiply those past their taps by zero
+    (0 * NaN = NaN), so ring slots a block never fills must hold zeros - r04 found NaN audio in
+    short-filter steps on fresh boxes before the ring was zeroed per launch."""
+    for rep in range(4):
+        _run(ops, orc, T, D, Ta, Da, 0, n_rf + 37 * rep, 0, seed=17 * T + rep, store=False, check_kernel=False,
+             poison=True)
