@@ -310,10 +310,15 @@ def kernel_compute(cls, n_out, T, D):
         s = (T + 62) // 32  # K-blocks of 32: K = 32 S >= T + 31
         return ("f16 MFMA (2 tap limbs, fp32 accumulate)", n_out * 2 * 2 * 32 * s * 2, F16_PEAK_TFLOPS)
     if cls in ("cf-mfma", "i8-dec-mfma"):
-        ks = -(-(-(-(31 * D + T) // 16)) // 8)  # K-steps of 16 per wave, 8 waves
+        ksteps = -(-(31 * D + T) // 16)  # Toeplitz K in steps of 16
+        if cls == "cf-mfma":  # 8 consumer waves, KS K-steps each
+            k_pad = 8 * 16 * -(-ksteps // 8)
+        else:  # r05 4-way kernel: the smallest instantiated K quarter that covers it (fir_i8_ws4.hip kW4KS)
+            need = -(-ksteps // 4)
+            k_pad = 4 * 16 * min(k for k in (2, 4, 6, 8, 11, 14, 17, 21, 22) if k >= need)
         prods = 3 if cls == "cf-mfma" else 2
-        return (f"f16 MFMA (split precision, {prods} products, padded Toeplitz K, fp32 accumulate)",
-                n_out * 2 * (8 * ks * 16) * prods * 2, F16_PEAK_TFLOPS)
+        return (f"f16 MFMA (split precision, {prods} products, padded Toeplitz K = {k_pad}, fp32 accumulate)",
+                n_out * 2 * k_pad * prods * 2, F16_PEAK_TFLOPS)
     return ("fp32 VALU FMA (direct form)", n_out * T * 4, FP32_PEAK_TFLOPS)
 
 
@@ -458,7 +463,7 @@ def cpu_baseline(wl, seconds_target=8.0):
 
 def kernel_name(chain):
     if isinstance(chain, AmChainSharded):
-        body = {"fft": "firFftKernel", "i8-dec-mfma": "firI8WsKernel", "valu": "firLdsKernel"}.get(
+        body = {"fft": "firFftKernel", "i8-dec-mfma": "firI8Ws4Kernel", "valu": "firLdsKernel"}.get(
             chain.kernel_class, chain.kernel_class)
         if chain.single:
             return (f"whole C5 step: gsdrInt8FirFCAmDemodFirFF ({body}<.., AUD>: RF FIR + AM + audio FIR in one "
@@ -471,7 +476,7 @@ def kernel_name(chain):
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"
     body = {"fft": "firFftD1PfKernel" if chain.D == 1 else "firFftKernel", "i8-mfma": "firI8MfmaKernel",
-            "i8-dec-mfma": "firI8WsKernel", "cf-mfma": "firCfWsKernel", "valu": "firLdsKernel"}[chain.kernel_class]
+            "i8-dec-mfma": "firI8Ws4Kernel", "cf-mfma": "firCfWsKernel", "valu": "firLdsKernel"}[chain.kernel_class]
     return f"{entry} ({body})"
 
 
@@ -858,6 +863,9 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the secondary measurements (C4 strong scaling, C5, C2, the C3 node path) that the "
                          "default run adds to its JSON line under 'extras'")
+    ap.add_argument("--kernel-policy", type=int, default=0,
+                    help="gsdrAmdSetKernelPolicy flags for A/B runs (e.g. 64 = GSDR_POLICY_I8_WS8, the r04 8-way int8 "
+                         "kernel); recorded in the line's config when nonzero")
     args = ap.parse_args()
     if args.share_gpu and args.backend != "gloo":
         raise SystemExit("bench.py: --share-gpu needs --backend gloo (RCCL runs one rank per GPU)")
@@ -869,6 +877,8 @@ def main():
     device = torch.device("cuda", local)
     stage = args.backend != "nccl"
     from gpusdr import ops
+    if args.kernel_policy:
+        ops.set_kernel_policy(args.kernel_policy)
     if args.workload == "c5":
         chain = (AmChainSharded(ops, rank, world, device, stage) if args.c5_mode == "sharded" else
                  AmChainRunner(ops, rank, world, device, args.c5_mode))
@@ -955,6 +965,7 @@ def main():
                                 f"{', ranks sharing cuda:0' if args.share_gpu else ''})")
                 if world > 1 else f"single GPU (halo = own history carry, {chain.geom.halo if chain.geom else 0} samples)",
                 "buffer_sets": getattr(chain, "n_slots", 1),
+                **({"kernel_policy": args.kernel_policy} if args.kernel_policy else {}),
                 **({"c5_mode": chain.mode, "audio_taps": chain.Ta, "audio_decimation": chain.Da}
                    if args.workload == "c5" else {}),
             },

@@ -308,6 +308,15 @@ uint32_t gspDriverGraphStats(gspHandle driver, size_t* eager, size_t* captured, 
   return Status_Success;
 }
 
+uint32_t gspDriverGraphDirectReplays(gspHandle driver, size_t* direct) {
+  IDriver* any = as<IDriver>(driver);
+  auto* d = dynamic_cast<gsdr_rt::SteppingDriver*>(any);
+  if (d == nullptr) d = gsdr_rt::componentSteppingDriver(any);
+  if (d == nullptr || direct == nullptr) return Status_InvalidArgument;
+  *direct = d->graphStats().direct;
+  return Status_Success;
+}
+
 uint32_t gspDriverSetFuseFirAm(gspHandle driver, int32_t on) {
   auto* d = dynamic_cast<gsdr_rt::SteppingDriver*>(as<IDriver>(driver));
   if (d == nullptr) return Status_InvalidArgument;

@@ -38,23 +38,12 @@
 
 #include "kcommon.h"
 #include "fir_launch.h"
+#include "ws_common.h"
 
 #include <gsdr/gsdr_amd.h>
 
 namespace gsdr_amd {
 
-typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef float v16f __attribute__((ext_vector_type(16)));
-
-constexpr int kCfWaves = 8;
-constexpr int kCfThreads = kCfWaves * kWave;
-constexpr int kCfTileOut = 512;  // 16 rows x 32 columns
-constexpr int kCfMaxKS = 11;     // K-steps of 16 per wave: K <= 8 x 11 x 16 = 1408
-constexpr int kCfMaxD = 16;
-constexpr int kCfPartialBytes = kCfWaves * 16 * kWave * 4;  // 32 KB
-constexpr int kCfDynLdsMax = 160 * 1024 - 256;             // the rest: static flags
 
 struct CfFirArgs {
   const float* x;     // interleaved re, im
@@ -74,7 +63,6 @@ struct CfFirArgs {
   uint32_t* abortOut;   // wave-specialised kernels: host-visible abort counter (wsAbortWord)
 };
 
-__device__ __forceinline__ int cfPhys(int u, int p) { return u + (u >> p); }
 
 // fp32 pair -> three bf16 limb pairs (exact).
 __device__ __forceinline__ void split3(float a, float b, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
@@ -627,165 +615,6 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfF16MfmaKernel(CfFirArgs a)
 // A producer's split of tile i + 1 runs on the vector ALUs while the consumers' MFMAs of tile i
 // run on the matrix cores of the same SIMDs.
 //
-// Hand-off counters (monotonic, one increment per wave): planesFull[set] (producers -> consumers:
-// tile's planes and mode written), planesFree[set] (consumers finished reading the set),
-// partsFull / partsFree (consumers among themselves: all partials of a tile written / all read),
-// pstat (producer-local statistics of the next tile published). Every wait is bounded: a wave that spins past the limit
-// raises `abort`, which releases every other wait, so the grid always drains.
-
-constexpr int kWsProducers = 4;
-constexpr int kWsPThreads = kWsProducers * kWave;           // 256
-constexpr int kWsThreads = kCfThreads + kWsPThreads;        // 768
-constexpr int kWsDirect = 0x7fffffff;                       // plane-set mode: direct fp32 tile
-constexpr int kWsSpinLimit = 1 << 22;                       // default s_sleep(1) iterations (~0.1 s)
-// Fused audio stage (firI8WsKernel<.., AUD>): AM ring of kAmRing tiles in LDS; the producers compute
-// the audio outputs of tile i - kAudioLag after producing the planes of tile i.
-constexpr int kAmRing = 8;
-constexpr int kAudioLag = 5;
-constexpr int kAmRingMirror = 256;  // ring[4096 + i] = ring[i] for i < 256: no wrap inside a window
-constexpr int kAudioMaxTaps = 256;  // 8 tap groups of 32 per output slot
-constexpr int kGWaves = 4;          // two-group kernel: consumer waves per group
-
-#ifndef GSDR_WS_WAITS
-#define GSDR_WS_WAITS 0
-#endif
-// hand-off polls: one LDS round trip each (1) or three (0, through r04)
-#ifndef GSDR_WS_POLL
-#define GSDR_WS_POLL 1
-#endif
-// fused audio stage: zero the AM ring per launch (0: the r04 defect, for its regression test only)
-#ifndef GSDR_WS_RING_ZERO
-#define GSDR_WS_RING_ZERO 1
-#endif
-// s_sleep argument between hand-off polls (units of 64 clocks; 0: spin on the LDS read alone)
-#ifndef GSDR_WS_SLEEP
-#define GSDR_WS_SLEEP 1
-#endif
-// int8 consumers with two partial buffers: tile i - 1's reduction interleaved with tile i's MFMAs
-// (r04: bit-identical and time-neutral, 171.7-172.9 vs 169.2-174.8 us per C5 launch; off)
-#ifndef GSDR_WS_RED_IL
-#define GSDR_WS_RED_IL 0
-#endif
-// int8 consumers: A-fragment reads in flight ahead of the MFMAs (K-steps)
-#ifndef GSDR_WS_PF
-#define GSDR_WS_PF 3
-#endif
-struct WsCtl {
-  int planesFull[2];
-  int planesFree[2];
-  int partsFull[2];                   // per partial buffer (one buffer: index 0)
-  int partsFree[2];
-  int pstat;
-  int tapsRead;                       // consumer waves done reading the taps staged in `part`
-  int amFull;                         // (unused since r04: per-slot counts, amSlot)
-  int amFree;                         // producer waves done with the audio outputs of a tile
-  int abort;
-  int mode[2];                        // per plane set: scale exponent sx, or kWsDirect
-  float stat[2][2][kWsProducers];     // [tile parity][max, smallest block max][producer wave]
-  int amSlot[kAmRing];                // fused audio stage: consumer waves' AM signals per ring slot
-  // set once by thread 0 (not part of the zeroed hand-off words above)
-  int spinLimit;
-  uint32_t* abortOut;
-};
-constexpr int kWsCtlZeroWords = (int)(offsetof(WsCtl, spinLimit) / 4);
-
-// Diagnostic builds only (-DGSDR_WS_DIAG=1, tools/gpu_r04_d.sh; the product build has none): bounds
-// checks on every index the fused audio stage and the AM ring writes compute, counted per kind, to
-// show whether the abort path (a wsWait that returns early) computes an index outside its range -
-// [0] audio-tile waits that returned on an abort, [1] history index outside
-// [0, amH), [2] block-local AM index outside the two ring tiles a window may span, [3] ring write
-// position outside the ring, [4] history reads, [5] ring reads.
-#ifndef GSDR_WS_DIAG
-#define GSDR_WS_DIAG 0
-#endif
-#if GSDR_WS_DIAG
-__device__ unsigned long long gWsDiag[8];
-__device__ __forceinline__ void wsDiag(int kind, bool hit) {
-  if (hit) atomicAdd(&gWsDiag[kind], 1ull);
-}
-#endif
-
-__device__ __forceinline__ void wsSignal(int* p, int lane) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS writes/reads complete
-  if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Hand-off wait profile, diagnostic builds only (-DGSDR_WS_WAITS=1; the product build has none): per
-// wave of the first 256 workgroups, the shader cycles spent in each kind of wait (the WsCtl counter
-// waited on) and the wave's whole span after its prologue, to tell which hand-off holds which role.
-// Kinds: 0 planesFull, 1 planesFree, 2 partsFull, 3 partsFree, 4 pstat, 5 tapsRead, 6 amFull,
-// 7 amFree; slot 8 = the wave's span, 9 = its wait count.
-#if GSDR_WS_WAITS
-constexpr int kWaitSlots = 10;
-__device__ unsigned long long gWsWaits[256 * 12 * kWaitSlots];
-__device__ __forceinline__ int wsWaitKind(const WsCtl* c, const int* p) {
-  const int off = (int)(p - reinterpret_cast<const int*>(c));  // WsCtl word index
-  return off < 2 ? 0 : off < 4 ? 1 : off < 6 ? 2 : off < 8 ? 3 : off == 8 ? 4 : off == 9 ? 5 : off == 10 ? 6 : 7;
-}
-// Consumer waves only (global atomics: the producers' counted vmcnt waits must not see extra
-// vector-memory operations, and the LDS has no room for per-wave counters); producers record their
-// span once, after their final vmcnt(0).
-__device__ __forceinline__ void wsWaitAdd(WsCtl*, int slot, unsigned long long v) {
-  const int wg = (int)blockIdx.x, w = (int)(threadIdx.x >> 6);
-  if (wg < 256 && w < kCfWaves && (threadIdx.x & 63) == 0) atomicAdd(&gWsWaits[(wg * 12 + w) * kWaitSlots + slot], v);
-}
-__device__ __forceinline__ void wsSpanStore(unsigned long long v) {
-  const int wg = (int)blockIdx.x, w = (int)(threadIdx.x >> 6);
-  if (wg < 256 && (threadIdx.x & 63) == 0) gWsWaits[(wg * 12 + w) * kWaitSlots + 8] = v;
-}
-#endif
-
-// A hand-off that never completes: release every other wait so the grid drains, and count the
-// failure where the host sees it (the entry points report it as hipErrorLaunchTimeOut). The count
-// goes through the global address space: a FLAT atomic would count on lgkmcnt too and turn every
-// later LDS wait of the wave into a full drain (lgkmcnt(0)).
-__device__ __forceinline__ void wsRaiseAbort(WsCtl* c) {
-  __hip_atomic_store(&c->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if ((threadIdx.x & (kWave - 1)) == 0 && c->abortOut != nullptr)
-    __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t*)(c->abortOut), 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
-#if GSDR_WS_WAITS
-  const unsigned long long t0w = __builtin_amdgcn_s_memtime();
-#endif
-#if GSDR_WS_POLL
-  // one LDS round trip per poll: the counter and the abort word read together, the spin limit
-  // once (reading the three one after the other, each waited for, made a poll ~3 round trips,
-  // added to the hand-off latency of every wait that polls)
-  if (waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target) {
-    const int lim = waveUniform(c->spinLimit);
-    for (int it = 0;; ++it) {
-      if (GSDR_WS_SLEEP > 0) __builtin_amdgcn_s_sleep(GSDR_WS_SLEEP);
-      const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const int ab = __hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (waveUniform(v) >= target || waveUniform(ab)) break;
-      if (it > lim) {
-        wsRaiseAbort(c);
-        break;
-      }
-    }
-  }
-#else
-  for (int it = 0;; ++it) {
-    const int v = waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (v >= target) break;
-    if (waveUniform(__hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
-    if (it > c->spinLimit) {
-      wsRaiseAbort(c);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-#endif
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#if GSDR_WS_WAITS
-  wsWaitAdd(c, wsWaitKind(c, p), __builtin_amdgcn_s_memtime() - t0w);
-  wsWaitAdd(c, 9, 1);
-#endif
-}
-
 // Producer window: G units (8 samples, 64 B) per producer thread, unit g = ptid + 256 j; only the
 // Wl units that hold window samples are loaded (the K padding beyond them stays zero in LDS).
 // Buffer loads against a per-tile descriptor whose range ends at the input's last byte: past the
@@ -797,7 +626,6 @@ __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
 // window in question is then complete while the 4 G loads issued after it stay in flight. (The
 // compiler's own counting merged both register windows at the loop header and waited for the
 // newer window's loads before every split.)
-typedef int i4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ i4v wsTileRsrc(const CfFirArgs& a, int tile, bool valid = true) {
   const int64_t first = (int64_t)tile * kCfTileOut * a.D;  // first window sample
@@ -1225,39 +1053,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
 
 // ---- int8 IQ input -------------------------------------------------------------------------
 
-struct I8DecArgs {
-  const int8_t* iq4;  // the input rounded down to 4 bytes; the samples start `sub` bytes later
-  const float* taps;
-  void* out;
-  int64_t nOut;
-  int64_t nIn;        // complex samples readable: (nOut - 1) D + T
-  int32_t sub;        // 0 or 2: byte offset of the first sample inside its dword
-  int32_t T;
-  int32_t D;
-  int32_t KS;
-  int32_t tiles;
-  int32_t Wu;         // window units (8 samples = 16 input bytes) per tile = 60 D + 16 KS
-  int32_t padShift;
-  int32_t planeStride;  // bytes between the I and Q f16 planes
-  int32_t dbp;          // wave-specialised kernel: two partial-sum buffers
-  int32_t spinLimit;    // as CfFirArgs
-  uint32_t* abortOut;
-  // fused audio stage (firI8WsKernel<.., true>): audio[j] = sum_t aTaps[t] A(j aD - amH + t) for
-  // j < aN, where A(k) is AM output k of this launch (k >= 0) or amHist[amH + k] (k < 0)
-  const float* aTaps;
-  float* aOut;
-  const float* amHist;
-  int64_t aN;
-  int32_t aT;
-  int32_t aD;
-  int32_t amH;
-  // two-group kernel (firI8WsGroupKernel): B fragments from shifted tap copies in LDS
-  int32_t kneed;     // K-steps of 16 that meet nonzero taps
-  int32_t tcLen;     // f16 elements per tap copy
-  int32_t tcStride;  // bytes between two tap-copy arrays (hi / lo limb of each shift)
-};
 
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 template <int G>
 struct I8DecWindow {
   uint32_t d[G][5];  // the dword holding the unit's first byte and the next four (a 2-byte-aligned
@@ -1416,178 +1212,6 @@ __global__ __launch_bounds__(kCfThreads, 1) void firI8DecMfmaKernel(I8DecArgs a)
 // misalignment and convert to the exact f16 I / Q planes (no statistics, no direct tiles);
 // consumers run two products per K-step and firI8DecMfmaKernel's epilogue (bit-identical).
 
-typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-
-template <int G>
-struct I8WsWindow {
-  u4v q[G];       // the unit's 16 bytes from the dword holding its first byte
-  uint32_t e[G];  // the next dword
-};
-
-__device__ __forceinline__ i4v wsI8TileRsrc(const I8DecArgs& a, int tile, bool valid) {
-  const int64_t first = (int64_t)tile * kCfTileOut * a.D * 2;  // bytes from iq4
-  const int64_t total = (2 * a.nIn + a.sub + 3) & ~(int64_t)3;  // whole dwords holding input bytes
-  const int64_t left = valid ? total - first : 0;
-  const int64_t bytes = left < 0x7fffffff ? left : 0x7fffffff;
-  const uint64_t base = reinterpret_cast<uint64_t>(a.iq4 + first);
-  i4v r;
-  r.x = waveUniform((int)(uint32_t)base);
-  r.y = waveUniform((int)((base >> 32) & 0xffffu));
-  r.z = waveUniform((int)bytes);
-  r.w = 0x00020000;
-  return r;
-}
-
-template <int G>
-__device__ __forceinline__ void wsI8LoadGroup(i4v rsrc, int Wl, int ptid, int j, I8WsWindow<G>& w) {
-  const int g = ptid + kWsPThreads * j;
-  const int voff = g < Wl ? 16 * g : 0x7ffffff0;
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(w.q[j]) : "v"(voff), "s"(rsrc) : "memory");
-  asm volatile("buffer_load_dword %0, %1, %2, 0 offen offset:16" : "=v"(w.e[j]) : "v"(voff), "s"(rsrc) : "memory");
-}
-
-template <int N, int G>
-__device__ __forceinline__ void wsI8WaitWindow(I8WsWindow<G>& w) {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-#pragma unroll
-  for (int j = 0; j < G; ++j) {
-    asm volatile("" : "+v"(w.q[j]));
-    asm volatile("" : "+v"(w.e[j]));
-  }
-}
-
-// Producer, tile i: wCur holds tile i's window (complete after the wait), wNext tile i + 1's.
-// `pre` runs while the window is still landing (the fused audio stage hides its work under that
-// wait; its few output stores sit behind tile i + 1's loads in the vmcnt order - issued a tile
-// earlier - and in front of tile i + 2's, so no window wait waits for loads issued this iteration).
-struct NoPre {
-  __device__ void operator()() const {}
-};
-
-template <int G, int NC = kCfWaves, typename Pre = NoPre>
-__device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
-                                                 int i, int ptid, I8WsWindow<G>& wCur, const Pre& pre = Pre{}) {
-  const int lane = ptid & (kWave - 1);
-  const int set = i & 1;
-  pre();
-  wsI8WaitWindow<2 * G>(wCur);
-  wsWait(c, &c->planesFree[set], NC * (i >> 1));
-  int8_t* planes = smem + set * 2 * a.planeStride;
-  const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
-#pragma unroll
-  for (int j = 0; j < G; ++j) {
-    const int g = ptid + kWsPThreads * j;
-    const uint32_t words[4] = {__builtin_amdgcn_alignbyte(wCur.q[j].y, wCur.q[j].x, a.sub),
-                               __builtin_amdgcn_alignbyte(wCur.q[j].z, wCur.q[j].y, a.sub),
-                               __builtin_amdgcn_alignbyte(wCur.q[j].w, wCur.q[j].z, a.sub),
-                               __builtin_amdgcn_alignbyte(wCur.e[j], wCur.q[j].w, a.sub)};
-    uint4 iu, qu;
-    int8IqToF16Units(words, iu, qu);
-    const int off = 16 * cfPhys(g < Wl ? g : a.Wu, a.padShift);  // spare unit Wu: never read
-    *reinterpret_cast<uint4*>(planes + off) = iu;
-    *reinterpret_cast<uint4*>(planes + a.planeStride + off) = qu;
-    wsI8LoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
-  }
-  if (ptid == 0) c->mode[set] = 0;
-  wsSignal(&c->planesFull[set], lane);
-}
-
-// Fused audio stage, producer side: the audio outputs of block-local tile t (global tile t0 + t) -
-// those whose window ends in that tile's AM range (tile 0 of the launch: also windows ending
-// before AM sample 0, in the history) - from the AM ring the consumers fill (tiles t - 1 and t are
-// in it: a window spans at most 256 AM samples), then amFree. A wave takes 8 outputs at a time,
-// jb + 4 o (o < 8, wave pw from jb = jLo + pw): lane l works on slot o = l / 8 with the taps
-// q + 8 u of its tap group q = l % 8 (u < 32; 32 LDS reads and FMAs, the 8 lanes of a slot reading
-// consecutive AM samples), then the slot's 8 partial sums meet in 3 DPP adds - no LDS round trip
-// (a 64-lane sum per output through ds_bpermute serialised ~50 LDS round trips per tile and made the
-// producers, who feed the matrix cores, the bottleneck: C5 0.18 -> 0.71 ms per step).
-// The lead tile (the previous block's last, computed for the ring only) has no outputs here.
-constexpr int kAudioTapsPerLane = kAudioMaxTaps / 8;
-
-
-template <int NSIG = kCfWaves>
-__device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* ring, WsCtl* c, int t0, bool lead, int t,
-                                            int ptid, const float (&ht)[kAudioTapsPerLane]) {
-  const int lane = ptid & (kWave - 1);
-  const int pw = ptid >> 6;
-  const int o = lane >> 3, q = lane & 7;
-  if (!(lead && t == 0)) {
-    // the ring slots of tiles t and t - 1 (a window spans at most 256 AM samples). Slot s holds
-    // tiles s, s + 8, ..., each signalled by the NSIG consumer waves that write it, and no slot is
-    // rewritten before the audio of the tile after its occupant is done (amFree), so a slot's count
-    // says exactly which of its tiles are complete. (A single tile counter, waited for at
-    // NSIG (t + 1), was not: a wave that reduced tile t + 1 could signal it before a slower wave
-    // had written its part of tile t - the count was reached with tile t incomplete. With short
-    // filters - 2 K-steps per wave, little MFMA work between the hand-offs - that happened: r04,
-    // test_am_chain_device_steps at T = 127 / D = 1 and T = 64 / D = 3.)
-    // Tile t - 1's slot was waited for by this wave's previous call (audio tiles run in order),
-    // except when that call was the lead tile's, which has no outputs and waits for nothing.
-    wsWait(c, &c->amSlot[t & (kAmRing - 1)], NSIG * (t / kAmRing + 1));
-    if (lead && t == 1) wsWait(c, &c->amSlot[0], NSIG);
-#if GSDR_WS_DIAG
-    wsDiag(0, lane == 0 && c->abort != 0);
-#endif
-    const int64_t g = (int64_t)(t0 + t);
-    // smallest j whose window end j aD - amH + aT - 1 is >= X
-    auto firstJ = [&](int64_t X) -> int64_t {
-      const int64_t num = X + a.amH - a.aT + 1;
-      return num <= 0 ? 0 : (num + a.aD - 1) / a.aD;
-    };
-    const int64_t jLo = g == 0 ? 0 : firstJ(g * kCfTileOut);
-    int64_t jHi = firstJ((g + 1) * kCfTileOut);
-    if (jHi > a.aN) jHi = a.aN;
-    for (int64_t jb = jLo + pw; jb < jHi; jb += 8 * kWsProducers) {
-      const int64_t j = jb + kWsProducers * o;
-      const int64_t k0 = j * a.aD - a.amH;  // this slot's window: AM samples k0 .. k0 + aT - 1
-      float s = 0.0f;
-      if (jb * a.aD - a.amH >= 0) {  // wave-uniform: every window of the batch lies in the ring
-        // block-local AM index, wrapped once: the mirror behind the ring keeps the window contiguous
-        // (immediate-offset LDS reads)
-        const float* w = ring + (((int)(k0 - (int64_t)kCfTileOut * t0) + q) & (kAmRing * kCfTileOut - 1));
-#if GSDR_WS_DIAG
-        if (j < jHi) {
-          const int64_t kk0 = k0 - (int64_t)kCfTileOut * t0 + q, kk1 = kk0 + 8 * (kAudioTapsPerLane - 1);
-          wsDiag(2, kk0 < 0 || kk0 < (int64_t)kCfTileOut * (t - 1) || kk1 >= (int64_t)kCfTileOut * (t + 1));
-          wsDiag(5, true);
-        }
-#endif
-#pragma unroll
-        for (int u = 0; u < kAudioTapsPerLane; ++u) s = fmaf(ht[u], w[8 * u], s);
-      } else {  // windows reaching into the history (the launch's first outputs)
-        // buffer loads (range-checked): a pointer select between the ring and the history would
-        // compile to FLAT loads
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.amHist), (short)0, 4 * a.amH,
-                                                          0x00020000);
-#pragma unroll 4
-        for (int u = 0; u < kAudioTapsPerLane; ++u) {
-          const int64_t k = k0 + q + 8 * u;
-          float x;
-#if GSDR_WS_DIAG
-          if (j < jHi) {
-            const int64_t kk = k - (int64_t)kCfTileOut * t0;
-            if (k >= 0) wsDiag(2, kk < 0 || kk < (int64_t)kCfTileOut * (t - 1) || kk >= (int64_t)kCfTileOut * (t + 1));
-            else wsDiag(1, a.amH + k < 0 || a.amH + k >= a.amH);
-            wsDiag(k >= 0 ? 5 : 4, true);
-          }
-#endif
-          if (k >= 0)
-            x = ring[(int)(k - (int64_t)kCfTileOut * t0) & (kAmRing * kCfTileOut - 1)];
-          else
-            x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * (a.amH + k)), 0, 0));
-          s = fmaf(ht[u], x, s);
-        }
-      }
-      // the slot's 8 tap groups: half-mirror, then the two quad swaps (every lane of the 8 ends
-      // with the sum)
-      s += dppF<0x141>(s);
-      s += dppF<0x4E>(s);
-      s += dppF<0xB1>(s);
-      if (q == 0 && j < jHi) a.aOut[j] = s;
-    }
-  }
-  wsSignal(&c->amFree, lane);
-}
-
 template <int KS, int G, int EPI, bool AUD = false>
 __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int Wl) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
@@ -1666,16 +1290,16 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
     }
     for (int i = 0;; i += 2) {
       wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
-        if (AUD && i >= kAudioLag) wsAudioTile(a8, ring, c, t0, lead, i - kAudioLag, ptid, ht);
+        if (AUD && i >= kAudioLag) wsAudioTile(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht);
       });
       if (i + 1 >= n) break;
       wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
-        if (AUD && i + 1 >= kAudioLag) wsAudioTile(a8, ring, c, t0, lead, i + 1 - kAudioLag, ptid, ht);
+        if (AUD && i + 1 >= kAudioLag) wsAudioTile(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht);
       });
       if (i + 2 >= n) break;
     }
     if constexpr (AUD)
-      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile(a8, ring, c, t0, lead, t, ptid, ht);
+      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile(a8, ring, c, t0, n, lead, t, ptid, ht);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if GSDR_WS_WAITS
     wsSpanStore(__builtin_amdgcn_s_memtime() - span0);
@@ -1900,16 +1524,16 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsGroupKernel(I8DecArgs a8
     }
     for (int i = 0;; i += 2) {
       wsI8ProducerTile<G, kGWaves>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
-        if (AUD && i >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, lead, i - kAudioLag, ptid, ht);
+        if (AUD && i >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht);
       });
       if (i + 1 >= n) break;
       wsI8ProducerTile<G, kGWaves>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
-        if (AUD && i + 1 >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, lead, i + 1 - kAudioLag, ptid, ht);
+        if (AUD && i + 1 >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht);
       });
       if (i + 2 >= n) break;
     }
     if constexpr (AUD)
-      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile<kGWaves>(a8, ring, c, t0, lead, t, ptid, ht);
+      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, t, ptid, ht);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }
@@ -1920,57 +1544,6 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsGroupKernel(I8DecArgs a8
 
 namespace {
 
-// Lane groups of ds_read_b128 (MI355X_MICROARCH.md, LDS): 4 x 16 lanes, one LDS cycle each.
-constexpr int kB128Groups[4][16] = {
-    {0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
-    {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
-    {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
-    {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
-
-struct CfLayout {
-  int padShift;
-  int planeStride;
-};
-
-// Pick the plane padding and the I/Q plane offset that minimise the A-fragment bank conflicts
-// for this (D, KS), within the LDS budget.
-CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes, size_t extra = kCfPartialBytes) {
-  CfLayout best{4, 0};
-  double bestCost = 1e30;
-  for (int p = 4; p >= 1; --p) {
-    const int units = Wu + (Wu >> p) + 1;
-    const int base = (16 * units + 255) / 256 * 256;
-    for (int qoff = 0; qoff < 16; ++qoff) {
-      const int stride = base + 16 * qoff;
-      if (nPlanes * (size_t)stride + extra > (size_t)kCfDynLdsMax) continue;
-      double cost = 0;
-      for (int s = 0; s < kCfWaves * KS; ++s) {
-        for (const auto& grp : kB128Groups) {
-          int slots[16][4];
-          int cnt[16] = {};
-          int worst = 1;
-          for (int li = 0; li < 16; ++li) {
-            const int l = grp[li];
-            const int u = 4 * D * (l & 15) + 2 * s + (l >> 5);
-            const int unit = u + (u >> p) + (((l >> 4) & 1) ? stride / 16 : 0);
-            const int slot = unit & 15;
-            bool dup = false;
-            for (int c = 0; c < cnt[slot]; ++c) dup |= slots[slot][c] == unit;
-            if (!dup && cnt[slot] < 4) slots[slot][cnt[slot]++] = unit;
-            worst = cnt[slot] > worst ? cnt[slot] : worst;
-          }
-          cost += worst;
-        }
-      }
-      cost += 1e-3 * (nPlanes * (double)stride) / 1024.0;  // tie-break: less LDS
-      if (cost < bestCost) {
-        bestCost = cost;
-        best = CfLayout{p, stride};
-      }
-    }
-  }
-  return best;
-}
 
 // F16: 0 = bf16 x 3, 1 = f16 x 2 single plane set, 2 = f16 x 2 double-buffered
 template <int F16, int KS, int G, int EPI>
@@ -2297,6 +1870,10 @@ hipError_t wsPrepare(hipStream_t stream, int32_t& spinLimit, uint32_t*& abortOut
 
 }  // namespace
 
+hipError_t wsPrepareLaunch(hipStream_t stream, int32_t& spinLimit, uint32_t*& abortOut) {
+  return wsPrepare(stream, spinLimit, abortOut);
+}
+
 bool firCfMfmaEligible(size_t tapCount, size_t decimation, const void* in) {
   const size_t d = decimation < 1 ? 1 : decimation;
   return tapCount >= 64 && d <= (size_t)kCfMaxD && 31 * d + tapCount <= (size_t)(kCfWaves * kCfMaxKS * 16) &&
@@ -2414,6 +1991,11 @@ hipError_t launchFirI8DecMfma(const int8_t* iq, const float* taps, size_t tapCou
   const uint32_t policy = kernelPolicy();
 #endif
   const int grid = (int)(tiles < 256 ? tiles : 256);
+  // the 4-way split-K kernel (r05) unless GSDR_POLICY_NO_WS / GSDR_POLICY_I8_WS8
+  if ((policy & (GSDR_POLICY_NO_WS | GSDR_POLICY_I8_WS8)) == 0) {
+    const hipError_t e = launchFirI8Ws4(a, ksteps, epi, false, stream);
+    if (e != hipErrorNotSupported) return e;
+  }
   // wave-specialised unless GSDR_POLICY_NO_WS (two plane sets of the int8 window always fit)
   const int Wl = std::min(a.Wu, (511 * a.D + a.T + 7) / 8);
   if ((policy & GSDR_POLICY_NO_WS) == 0 && Wl <= 4 * kWsPThreads) {
@@ -2522,6 +2104,18 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
     layCache.emplace_back(key, l);
     return l;
   };
+  if ((policy & GSDR_POLICY_I8_WS8) == 0) {  // the 4-way split-K kernel (r05)
+    I8DecArgs w = a;
+    w.aTaps = aTaps;
+    w.aOut = aOut;
+    w.amHist = amHist;
+    w.aN = (int64_t)aN;
+    w.aT = (int32_t)aT;
+    w.aD = (int32_t)aD;
+    w.amH = (int32_t)amH;
+    const hipError_t e = launchFirI8Ws4(w, ksteps, kEpiAm, true, stream);
+    if (e != hipErrorNotSupported) return e;
+  }
   const size_t ringBytes = sizeof(float) * (kAmRing * kCfTileOut + kAmRingMirror);
 #if GSDR_WS_GROUPS
   // the two-group kernel (bit-identical outputs; GSDR_POLICY_NO_WS_GROUPS keeps the 8-way one)
@@ -2579,6 +2173,9 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
 }  // namespace gsdr_amd
 
 #if GSDR_WS_WAITS
+namespace gsdr_amd {
+hipError_t w4WaitsRead(unsigned long long* out, size_t n, int reset);
+}
 extern "C" __attribute__((visibility("default"))) hipError_t gsdrAmdWsWaits(unsigned long long* out, size_t count,
                                                                              int reset) {
   hipError_t e = hipDeviceSynchronize();
@@ -2589,11 +2186,15 @@ extern "C" __attribute__((visibility("default"))) hipError_t gsdrAmdWsWaits(unsi
     e = hipGetSymbolAddress(&p, HIP_SYMBOL(gsdr_amd::gWsWaits));
     if (e == hipSuccess) e = hipMemset(p, 0, sizeof(unsigned long long) * 256 * 12 * gsdr_amd::kWaitSlots);
   }
+  if (e == hipSuccess) e = gsdr_amd::w4WaitsRead(out, n, reset);  // the 4-way kernel's unit
   return e;
 }
 #endif
 
 #if GSDR_WS_DIAG
+namespace gsdr_amd {
+hipError_t w4DiagRead(unsigned long long* out8, int reset);
+}
 extern "C" __attribute__((visibility("default"))) hipError_t gsdrAmdWsDiag(unsigned long long* out8, int reset) {
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(gsdr_amd::gWsDiag), 8 * sizeof(unsigned long long));
@@ -2601,6 +2202,7 @@ extern "C" __attribute__((visibility("default"))) hipError_t gsdrAmdWsDiag(unsig
     const unsigned long long z[8] = {};
     e = hipMemcpyToSymbol(HIP_SYMBOL(gsdr_amd::gWsDiag), z, sizeof z);
   }
+  if (e == hipSuccess) e = gsdr_amd::w4DiagRead(out8, reset);  // the 4-way kernel's unit
   return e;
 }
 #endif

@@ -346,7 +346,15 @@ __device__ __forceinline__ void loadTw(f2 (&t)[7], const Lds& L, int stage) {
   for (int kp = 0; kp < 4; ++kp) {
     const f4 v = L.tw[(stage * 4 + kp) * 64];
     t[2 * kp] = f2{v.x, v.y};
-    if (2 * kp + 1 < 7) t[2 * kp + 1] = f2{v.z, v.w};
+    if (2 * kp + 1 < 7) {
+      t[2 * kp + 1] = f2{v.z, v.w};
+    } else {
+      // keep the unused slot 7 live: a whole ds_read_b128 (lanes 16 B apart, conflict free). Loading
+      // only t[6], the compiler paired two stages' 8-byte reads into ds_read2st64_b64, whose 16-lane
+      // accesses 16 B apart hit every bank pair twice (r05: 2-way conflicts in every FFT)
+      float zw0 = v.z, zw1 = v.w;
+      asm volatile("" : "+v"(zw0), "+v"(zw1));
+    }
   }
 }
 
@@ -410,13 +418,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t blockRsrc(const void* base, in
 
 // cf32 row-group image: row r of the group at 16-byte unit r kRowUnits<D> (D / 2 units of data).
 // Rows D * 8 bytes apart put the ds_read_b128 of lanes 64 / (D / 2) apart on the same banks when D / 2
-// is a power of two (D = 8, the D = 1 kernel: 4-way, 15 % of its LDS cycles in SQ_LDS_BANK_CONFLICT);
-// one pad unit per row then spreads a 16-lane group over 16 distinct bank quads.
+// is a power of two (D = 8, the D = 1 kernel: 4-way, 15 % of its LDS cycles in SQ_LDS_BANK_CONFLICT).
+// D = 4: one pad unit per row spreads a 16-lane group over 16 distinct bank quads. D = 8 (r05): no pad,
+// the units of row r XOR-swizzled by (r >> 2) & 3 instead - the padded image (5 units per row) left the
+// ds_write_b128 of the transposition 2-way conflicted (8-lane groups over 32 banks: lanes 0 and 7 of
+// every group on one bank quad), 8 extra LDS cycles per write, ~260 of the D = 1 kernel's ~350 conflict
+// cycles per block (SQ_LDS_BANK_CONFLICT 11.6 % of SQ_LDS_IDX_ACTIVE, r04). With the swizzle a write's
+// 8 lanes cover two whole consecutive rows (32 distinct banks) and a ds_read_b128 lane group's 16 lanes
+// hit 16 distinct bank quads (the four lanes of a group that share l mod 4 get four distinct swizzles).
 #ifndef GSDR_FFT_PADROWS
 #define GSDR_FFT_PADROWS 1
 #endif
 template <int D>
-constexpr int kRowUnits = D / 2 + ((GSDR_FFT_PADROWS && (D == 4 || D == 8)) ? 1 : 0);
+constexpr int kRowUnits = D / 2 + ((GSDR_FFT_PADROWS && D == 4) ? 1 : 0);
+template <int D>
+__device__ __forceinline__ int rowSwizzle(int row) {
+  return D == 8 ? (row >> 2) & 3 : 0;
+}
 
 template <int D>
 constexpr int scratchComplex(int input) {
@@ -548,7 +566,8 @@ __device__ __forceinline__ void transposeRows(Rows<D, kCf32>& R, f2* s, int l) {
 #pragma unroll
       for (int i = 0; i < H; ++i) {  // unit u = 64 i + l of the group: row u / H, unit u % H of it
         const int u = i * 64 + l;
-        s4[RU == H ? u : (u / H) * RU + u % H] = f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
+        s4[RU == H ? (u ^ rowSwizzle<D>(u / H)) : (u / H) * RU + u % H] =
+            f4{R.v[j][2 * i].x, R.v[j][2 * i].y, R.v[j][2 * i + 1].x, R.v[j][2 * i + 1].y};
       }
     }
     ldsOrder();
@@ -558,7 +577,7 @@ __device__ __forceinline__ void transposeRows(Rows<D, kCf32>& R, f2* s, int l) {
       const int j = j0 + g;
 #pragma unroll
       for (int p = 0; p < D; p += 2) {  // row l: 16-byte reads (D even), lanes 16 RU bytes apart
-        const f4 u = s4[l * RU + p / 2];
+        const f4 u = s4[l * RU + ((p / 2) ^ rowSwizzle<D>(l))];
         R.v[j][p] = f2{u.x, u.y};
         R.v[j][p + 1] = f2{u.z, u.w};
       }

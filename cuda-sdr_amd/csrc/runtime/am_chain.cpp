@@ -24,6 +24,7 @@
 // the pinned-ring mode it runs on a second stream, ordered by events against the step that last
 // read staging[p], so it overlaps the previous step's compute.
 #include <gsdr/gsdr_amd.h>
+#include <gpusdrpipeline/GSLog.h>
 
 #include <hip/hip_runtime.h>
 
@@ -460,6 +461,28 @@ hipError_t gsdrAmChainStepResident(gsdrAmChain c, const int8_t* inputIq, size_t 
     c->resident = nullptr;
   }
   const bool firstStep = c->steps == 0;
+  // The launch reads [inputIq - 2 r, inputIq + 2 L nChunks) after the first step (the RF history in
+  // place) and [inputIq, ...) on it: both must lie inside inputIq's device allocation. A non-first step
+  // handed a pointer with no room for its history in front read before the allocation and faulted the
+  // GPU (r04, tools/exp/ws_abort_diag.py); it is now rejected with hipErrorInvalidValue instead.
+  {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    const auto p = reinterpret_cast<uintptr_t>(inputIq);
+    if (hipMemGetAddressRange(&base, &size, const_cast<int8_t*>(inputIq)) != hipSuccess || base == nullptr) {
+      (void)hipGetLastError();
+      gsloge("gsdrAmChainStepResident: inputIq is not device memory of this process");
+      return hipErrorInvalidValue;
+    }
+    const auto lo = reinterpret_cast<uintptr_t>(base), hi = lo + size;
+    const size_t before = firstStep ? 0 : 2 * c->r;
+    if (p - lo < before || p + 2 * c->L * nChunks > hi) {
+      gsloge("gsdrAmChainStepResident: the %s of this step lies outside inputIq's allocation (%zu bytes in front, "
+             "%zu needed; %zu after, %zu needed)", p - lo < before ? "RF history in front" : "input",
+             (size_t)(p - lo), before, (size_t)(hi - p), (size_t)(2 * c->L * nChunks));
+      return hipErrorInvalidValue;
+    }
+  }
   if (c->resident == nullptr || c->resIn != inputIq || c->resOut != output || c->resChunks != nChunks ||
       c->resFirst != firstStep) {
     if (c->resident) (void)hipGraphExecDestroy(c->resident);

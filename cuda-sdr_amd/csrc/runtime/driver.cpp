@@ -460,6 +460,7 @@ Status SteppingDriver::doFilterGraphed(hipStream_t stream) noexcept {
       } else {
         for (const hipKernelNodeParams& k : g.kernels)
           SAFE_HIP_OR_RET_STATUS(hipLaunchKernel(k.func, k.gridDim, k.blockDim, k.kernelParams, k.sharedMemBytes, stream));
+        ++mStats.direct;
       }
       ++mStats.replayed;
       mGraphMisses = 0;

@@ -55,6 +55,7 @@ class SteppingDriver final : public ISteppingDriver {
     size_t eager = 0;     // steps run as plain launches
     size_t captured = 0;  // steps that captured (and launched) a new graph
     size_t replayed = 0;  // steps whose device work was a cached graph launch
+    size_t direct = 0;    // of those: replayed as direct kernel launches (a linear chain of kernel nodes)
     size_t fused = 0;     // Fir -> QuadAmDemod edges moved as one fused launch
   };
   GraphStats graphStats() const noexcept { return mStats; }

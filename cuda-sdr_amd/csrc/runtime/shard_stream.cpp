@@ -105,7 +105,8 @@ struct gsdrShardStreamImpl {
   hipStream_t xstream = nullptr;
   hipEvent_t segReady = nullptr, exchanged = nullptr;
   hipEvent_t stepDone = nullptr;  // the last step's completion on its stream (Destroy waits for it)
-  bool stepped = false;
+  bool stepped = false;      // stepDone marks the end of the last enqueued step
+  bool syncDevice = false;   // a failed step's end could not be recorded: destroy synchronises the device
   bool ring = false;              // the ring protocol (world > 1, or a ring of one with a hook)
   gsdrHaloExchangeFn exchange = nullptr;
   void* user = nullptr;
@@ -196,7 +197,8 @@ GSDR_API void gsdrShardStreamDestroy(gsdrShardStream s) {
     // waited for the exchange) and the exchange stream itself - not the whole device, which would
     // stall every other stream of the application
     DevicePush push(s->device);
-    if (s->stepped) (void)hipEventSynchronize(s->stepDone);
+    if (s->syncDevice) (void)hipDeviceSynchronize();
+    else if (s->stepped) (void)hipEventSynchronize(s->stepDone);
     if (s->xstream) (void)hipStreamSynchronize(s->xstream);
   }
   s->release();
@@ -209,18 +211,14 @@ GSDR_API void* gsdrShardStreamHalo(gsdrShardStream s) { return s == nullptr ? nu
 
 GSDR_API size_t gsdrShardStreamOutputCount(gsdrShardStream s) { return s == nullptr ? 0 : s->outputs; }
 
-GSDR_API hipError_t gsdrShardStreamStep(gsdrShardStream s, void* output, hipStream_t stream) {
-  if (s == nullptr || output == nullptr) return hipErrorInvalidValue;
-  DevicePush push(s->device);
-  if (!push.ok) return hipErrorInvalidDevice;
-  auto* out = static_cast<uint8_t*>(output);
+// One step's enqueues; the caller records the step's end whatever this returns.
+static hipError_t shardStep(gsdrShardStream s, uint8_t* out, hipStream_t stream, bool& enqueued) {
   uint8_t* tail = s->buf + s->L * s->elem;  // segment[L - H, L) = buf[L, L + H)
   const size_t haloBytes = s->H * s->elem;
+  enqueued = true;  // from here on work of this step may be queued on `stream` / xstream
   if (!s->ring) {
     SHS_TRY(s->fir(s->buf, s->outputs, out, stream));
     if (haloBytes > 0) SHS_TRY(hipMemcpyAsync(s->buf, tail, haloBytes, hipMemcpyDeviceToDevice, stream));
-    SHS_TRY(hipEventRecord(s->stepDone, stream));
-    s->stepped = true;
     return hipSuccess;
   }
   uint8_t* dst = s->rank == 0 ? s->incoming : s->buf;
@@ -238,9 +236,24 @@ GSDR_API hipError_t gsdrShardStreamStep(gsdrShardStream s, void* output, hipStre
     SHS_TRY(hipStreamWaitEvent(stream, s->exchanged, 0));
     SHS_TRY(s->fir(s->buf, s->head, out, stream));
   }
-  SHS_TRY(hipEventRecord(s->stepDone, stream));
-  s->stepped = true;
   return hipSuccess;
+}
+
+GSDR_API hipError_t gsdrShardStreamStep(gsdrShardStream s, void* output, hipStream_t stream) {
+  if (s == nullptr || output == nullptr) return hipErrorInvalidValue;
+  DevicePush push(s->device);
+  if (!push.ok) return hipErrorInvalidDevice;
+  bool enqueued = false;
+  const hipError_t e = shardStep(s, static_cast<uint8_t*>(output), stream, enqueued);
+  if (enqueued) {
+    // every exit after the first enqueue - a failed launch or exchange included - marks the step's end,
+    // so destroy waits for whatever of it was queued. Where even that fails, destroy
+    // falls back to a device synchronisation.
+    if (s->ring) (void)hipStreamWaitEvent(stream, s->exchanged, 0);
+    if (hipEventRecord(s->stepDone, stream) == hipSuccess) s->stepped = true;
+    else s->syncDevice = true;
+  }
+  return e;
 }
 
 GSDR_API hipError_t gsdrShardExchangeRccl(void* ncclComm, const void* sendTail, void* recvHalo, size_t bytes,

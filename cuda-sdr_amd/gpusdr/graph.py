@@ -72,6 +72,7 @@ def _L():
             "gspDriverDoFilter": ([h], u32),
             "gspDriverDoFilterGraphed": ([h, h], u32),
             "gspDriverGraphStats": ([h, psz, psz, psz], u32),
+            "gspDriverGraphDirectReplays": ([h, psz], u32),
             "gspDriverNodeName": ([h, h, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int32)], sz),
         }
         for name, (args, res) in sigs.items():
@@ -198,9 +199,10 @@ class Node(_Handle):
 
     def graph_stats(self):
         """A JSON Component's inner stepping: plain, capturing and replayed steps (hipGraph)."""
-        e, c, r = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        e, c, r, d = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
         _check(_L().gspDriverGraphStats(self._h, ctypes.byref(e), ctypes.byref(c), ctypes.byref(r)), "graphStats")
-        return {"eager": e.value, "captured": c.value, "replayed": r.value}
+        _check(_L().gspDriverGraphDirectReplays(self._h, ctypes.byref(d)), "graphDirectReplays")
+        return {"eager": e.value, "captured": c.value, "replayed": r.value, "direct": d.value}
 
     # -- constructors mirroring the reference factories --
     @classmethod
@@ -311,10 +313,11 @@ class SteppingDriver(_Handle):
         _check(_L().gspDriverDoFilterGraphed(self._h, queue.handle), "doFilterGraphed")
 
     def graph_stats(self):
-        e, c, r, f = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        e, c, r, f, d = (ctypes.c_size_t() for _ in range(5))
         _check(_L().gspDriverGraphStats(self._h, ctypes.byref(e), ctypes.byref(c), ctypes.byref(r)), "graphStats")
         _check(_L().gspDriverFusedSteps(self._h, ctypes.byref(f)), "fusedSteps")
-        return {"eager": e.value, "captured": c.value, "replayed": r.value, "fused": f.value}
+        _check(_L().gspDriverGraphDirectReplays(self._h, ctypes.byref(d)), "graphDirectReplays")
+        return {"eager": e.value, "captured": c.value, "replayed": r.value, "fused": f.value, "direct": d.value}
 
     def set_fuse_fir_am(self, on: bool):
         """Fir -> QuadAmDemod as one fused launch (default on; off = the reference's two launches)."""

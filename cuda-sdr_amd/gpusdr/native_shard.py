@@ -73,6 +73,8 @@ class RcclComm:
         if len(uid) != 128:
             raise ValueError("an ncclUniqueId is 128 bytes")
         self._uid = ctypes.create_string_buffer(uid, 128)
+        self._users = 0  # ShardStreams whose exchange hook holds this communicator
+        self.handle = ctypes.c_void_p(None)
         h = ctypes.c_void_p()
         _rccl_check(_L().gsdrShardRcclCommCreate(int(nranks), self._uid, int(rank), int(device), ctypes.byref(h)),
                     "gsdrShardRcclCommCreate")
@@ -84,9 +86,23 @@ class RcclComm:
                                                xstream), "gsdrShardExchangeRccl")
 
     def close(self):
+        """Destroy the communicator. Refused while a ShardStream still uses it (the executor
+        would keep a dangling ncclComm_t, with RCCL work possibly queued on its exchange stream): close
+        those streams first."""
+        if self._users > 0:
+            raise RuntimeError(f"RcclComm.close: {self._users} ShardStream(s) still use this communicator; "
+                               "close them first")
         if self.handle:
             _rccl_check(_L().gsdrShardRcclCommDestroy(self.handle), "gsdrShardRcclCommDestroy")
             self.handle = ctypes.c_void_p(None)
+
+    def __del__(self):
+        # a ShardStream keeps a reference to its communicator, so by the time this runs none uses it
+        try:
+            if self._users == 0:
+                self.close()
+        except Exception:
+            pass
 
 
 def host_staged_exchange(group=None):
@@ -133,9 +149,14 @@ class ShardStream:
                 return 999  # hipErrorUnknown
 
         user = None
+        self._comm = None
+        self._h = ctypes.c_void_p(None)
         if isinstance(exchange, RcclComm):  # the native hook itself, user = the communicator
+            if not exchange.handle:
+                raise ValueError("ShardStream: the RcclComm is closed")
             self._cb = ctypes.cast(_L().gsdrShardExchangeRccl, EXCHANGE_FN)
             user = exchange.handle
+            self._comm = exchange  # kept alive (and its close() refused) until this stream is closed
         else:
             self._cb = EXCHANGE_FN(trampoline) if exchange is not None else EXCHANGE_FN()
         h = ctypes.c_void_p()
@@ -143,12 +164,19 @@ class ShardStream:
                                          self.taps.ctypes.data, len(self.taps), self.D, self.L, self._cb, user,
                                          self.device, ctypes.byref(h)), "gsdrShardStreamCreate")
         self._h = h
+        if self._comm is not None:
+            self._comm._users += 1
         self.outputs = _L().gsdrShardStreamOutputCount(h)
 
     def close(self):
+        """Destroy the executor (it waits for its own queued steps and exchanges), then release the
+        communicator it used."""
         if self._h:
             _L().gsdrShardStreamDestroy(self._h)
             self._h = ctypes.c_void_p(None)
+            if self._comm is not None:
+                self._comm._users -= 1
+                self._comm = None
 
     def __del__(self):
         try:

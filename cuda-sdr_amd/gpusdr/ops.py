@@ -185,10 +185,11 @@ def am_chain_fused(taps: torch.Tensor, iq: torch.Tensor, decimation: int, rf_cou
     return audio_out
 
 
-def poison_lds(device: int = 0, pattern: int = 0x7FC00000) -> None:
-    """gsdrAmdPoisonLds on the current stream (tests: stale-LDS reads become visible)."""
-    check(lib().gsdrAmdPoisonLds(pattern, device, ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)),
-          "gsdrAmdPoisonLds")
+def poison_lds(device: int = 0, pattern: int = 0x7FC00000, stream=None) -> None:
+    """gsdrAmdPoisonLds on `stream` (a torch stream; default: the current stream) - tests: stale-LDS
+    reads become visible."""
+    s = torch.cuda.current_stream(device) if stream is None else stream
+    check(lib().gsdrAmdPoisonLds(pattern, device, ctypes.c_void_p(s.cuda_stream)), "gsdrAmdPoisonLds")
 
 
 def hbm_probe(src: torch.Tensor, dst: torch.Tensor, mode: int) -> None:
@@ -280,6 +281,7 @@ POLICY_CF_BF16 = 2  # GSDR_POLICY_CF_BF16
 POLICY_NO_WS = 4  # GSDR_POLICY_NO_WS: barrier-synchronous decimating MFMA kernels
 POLICY_NO_FFT = 8  # GSDR_POLICY_NO_FFT: long real-tap FIRs on the direct forms, not the FFT kernel
 POLICY_PREFER_FFT = 16  # GSDR_POLICY_PREFER_FFT: int8 IQ on the FFT kernel even where int8 MFMA applies
+POLICY_I8_WS8 = 64  # GSDR_POLICY_I8_WS8: int8 decimating FIRs on the r04 8-way wave-specialised kernel
 
 
 def set_kernel_policy(flags: int) -> int:

@@ -107,6 +107,9 @@ GSP_API uint32_t gspDriverDoFilter(gspHandle driver);
  * gspDriverGraphStats counts plain, capturing and replayed steps. */
 GSP_API uint32_t gspDriverDoFilterGraphed(gspHandle driver, gspHandle queue);
 GSP_API uint32_t gspDriverGraphStats(gspHandle driver, size_t* eager, size_t* captured, size_t* replayed);
+/* Of the replayed steps: those replayed as direct kernel launches (the captured graph was a linear chain
+ * of kernel nodes); the rest went through hipGraphLaunch. */
+GSP_API uint32_t gspDriverGraphDirectReplays(gspHandle driver, size_t* direct);
 /* Fir -> QuadAmDemod fusion (on by default): a Fir with real taps whose only sink is a QuadAmDemod
  * on the same queue is stepped with it as ONE gsdrFirFCAmDemod launch (the same envelopes within
  * the FIR tolerance: the fused launch covers a different span, which moves the FFT / matrix-core

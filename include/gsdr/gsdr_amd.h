@@ -147,6 +147,10 @@ GSDR_API hipError_t gsdrFmDemod(size_t rfSampleRate, float tunedFrequency, float
 /* int8 IQ input takes the FFT fast convolution even where the int8 MFMA kernels apply (by default
  * they do: faster for int8 at the C5 shape); A/B comparisons and tests of the int8 FFT path. */
 #define GSDR_POLICY_PREFER_FFT 16u
+/* int8 IQ decimating MFMA FIRs (and the fused C5 chain) on the 8-way split-K wave-specialised kernel of
+ * r01-r04 instead of the 4-way one (r05: one consumer wave per SIMD); A/B
+ * comparisons. (32u is taken by experimental builds.) */
+#define GSDR_POLICY_I8_WS8 64u
 GSDR_API void gsdrAmdSetKernelPolicy(uint32_t flags);
 /* The kernel family the FC FIR entry points pick for this shape under the current policy:
  * "fft", "i8-mfma", "i8-dec-mfma", "cf-mfma" or "valu" (diagnostics / benchmark labels). */

@@ -107,6 +107,22 @@ def test_library_matches_source_tree(built):
     _check_build_id(built)
 
 
+def test_build_id_folds_in_compile_flags():
+    """the id covers EXTRA_FLAGS (the -D switches of A/B and diagnostic builds) and
+    the target, so a library built with, e.g., -DGSDR_WS_RING_ZERO=0 (the r04 stale-LDS defect) cannot
+    pass test_library_matches_source_tree; whitespace in the flags does not change it."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from source_hash import source_hash
+    product = source_hash(REPO)
+    assert source_hash(REPO, extra_flags="-DGSDR_WS_RING_ZERO=0") != product
+    assert source_hash(REPO, extra_flags="-DGSDR_WS_DIAG=1") != product
+    assert source_hash(REPO, arch="gfx942") != product
+    assert source_hash(REPO, extra_flags="  ") == product
+    # the Makefile's stamp makes every object depend on the flags, and the id is computed with them
+    mk = open(os.path.join(REPO, "cuda-sdr_amd", "Makefile")).read()
+    assert "--extra-flags='$(EXTRA_FLAGS)'" in mk and "$(FLAGSTAMP)" in mk
+
+
 @pytest.mark.gpu
 def test_gpu_box_library_matches_source_tree():
     """The same check where the GPU suite runs: the pushed, prebuilt .so the box loads must be the one

@@ -507,9 +507,43 @@ def test_replay_skips_host_step_and_matches_eager(graph, orc):
         if mode == "graphed":
             st = drv.graph_stats()
             assert st["replayed"] >= steps // 2, st
+            # the step holds a D2H memcpy node: replayed through hipGraphLaunch, never as direct launches
+            assert st["direct"] == 0, st
     assert outs["graphed"].tobytes() == outs["eager"].tobytes()
     assert len(outs["eager"]) > 0
     assert host["graphed"] < host["eager"], host
+
+
+def test_fused_step_replays_as_direct_launch(graph, orc):
+    """which replay path ran is observable. A steady-state fused Fir -> QuadAmDemod step into
+    a DeviceSink captures as ONE kernel node and is replayed by launching that kernel with its captured
+    parameters (no hipGraphLaunch): every replay is counted as direct; the chain's last Fir input window
+    then holds exactly the unconsumed history, as eager stepping leaves it."""
+    queue = graph.Queue.named("qdr")
+    T, D, per, steps = 1023, 10, 8192, 24
+    taps = orc.lowpass_taps(T, 0.04)
+    rng = np.random.default_rng(7)
+    left = {}
+    for mode in ("eager", "graphed"):
+        fir = graph.Node.fir(queue, taps, D, graph.SAMPLE_FLOAT_COMPLEX)
+        am = graph.Node.quad_am_demod(queue)
+        sink = graph.Node.from_json("DeviceSink", '{"commandQueue": "qdr", "preferredBytes": %d}' % (4 * per), queue)
+        drv = graph.SteppingDriver()
+        drv.connect(fir, 0, am, 0)
+        drv.connect(am, 0, sink, 0)
+        fir.push(np.zeros(T - 1, np.complex64))
+        for s in range(steps):
+            x = (rng.standard_normal(per * D) + 1j * rng.standard_normal(per * D)).astype(np.complex64)
+            fir.push(x)
+            drv.do_filter() if mode == "eager" else drv.do_filter_graphed(queue)
+        queue.sync()
+        left[mode] = fir.output_size()[0]
+        st = drv.graph_stats()
+        if mode == "graphed":
+            assert st["replayed"] >= 4 and st["direct"] == st["replayed"], st
+        else:
+            assert st["replayed"] == 0 and st["direct"] == 0, st
+    assert left["graphed"] == left["eager"]
 
 
 @pytest.mark.parametrize("elem,T,D", [("c", 1023, 10), ("c", 127, 1), ("i8", 1023, 10), ("i8", 127, 1)])

@@ -309,26 +309,33 @@ def test_int8_decimating_mfma_path(ops, orc, T, D, n_out):
 @pytest.mark.parametrize("T,D,n_out,off", [(1023, 10, 400_000, 0), (1023, 10, 130_001, 2), (255, 4, 200_000, 6),
                                            (1346, 2, 150_000, 0), (64, 3, 90_000, 4)])
 def test_int8_decimating_wave_specialised_bit_exact(ops, orc, T, D, n_out, off):
-    """The wave-specialised int8 decimating kernel (producer waves convert, consumer waves run the
-    MFMAs) is bit-identical to the barrier-synchronous one, at several tiles per block and at
-    2-byte-misaligned inputs; and within tolerance of float64 on a prefix."""
+    """The r01-r04 8-way wave-specialised int8 decimating kernel (GSDR_POLICY_I8_WS8: producer waves
+    convert, 8 consumer waves split K) is bit-identical to the barrier-synchronous one, at several tiles
+    per block and at 2-byte-misaligned inputs. The default 4-way kernel (r05: one consumer wave per SIMD,
+    a quarter of K each) groups the K sums differently: it is within the float64 bound on a prefix, and
+    within twice it of the synchronous kernel everywhere."""
     rng = np.random.default_rng(T + D + off)
     n_in = (n_out - 1) * D + T
     iq = rng.integers(-128, 128, size=2 * n_in + off).astype(np.int8)
     taps = orc.lowpass_taps(T, 0.4 / D).astype(np.float32)
     iq_d, taps_d = _dev(iq)[off:], _dev(taps)
     for am in (False, True):
-        with _Policy(ops, ops.POLICY_NO_FFT):
-            y_ws = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=am))
+        with _Policy(ops, ops.POLICY_NO_FFT | ops.POLICY_I8_WS8):
+            y_ws8 = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=am))
         with _Policy(ops, ops.POLICY_NO_WS | ops.POLICY_NO_FFT):
             y_sync = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True, am=am))
-        assert y_ws.tobytes() == y_sync.tobytes(), ("i8-ws-vs-sync", T, D, n_out, off, am)
+        assert y_ws8.tobytes() == y_sync.tobytes(), ("i8-ws8-vs-sync", T, D, n_out, off, am)
     m = min(n_out, 5000)
     x = orc.int8_to_float(iq[off: off + 2 * ((m - 1) * D + T)]).view(np.complex64)
     y64, bound = orc.fir_f64(taps, x, D, m)
     with _Policy(ops, ops.POLICY_NO_FFT):
-        y_ws = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))[:m]
-    _check_fir(y_ws, y64, bound, ("i8-ws", T, D, off))
+        y_ws = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))
+    _check_fir(y_ws[:m], y64, bound, ("i8-ws4", T, D, off))
+    with _Policy(ops, ops.POLICY_NO_FFT | ops.POLICY_I8_WS8):
+        y_ws8 = _host(ops.fir(taps_d, iq_d, D, n_out, int8_iq=True))
+    _check_fir(y_ws8[:m], y64, bound, ("i8-ws8", T, D, off))
+    # everywhere: |y4 - y8| <= 2e-6 sum|h||x|, sum|h||x| <= sum|h| max|x| (max |x| = 1 after the convert)
+    assert np.max(np.abs(y_ws - y_ws8)) <= 2 * FIR_TOL * np.abs(taps).sum() * 1.01, ("i8-ws4-vs-ws8", T, D)
 
 
 def test_int8_decimating_mfma_misaligned(ops, orc):

@@ -90,9 +90,18 @@ def _rank_main(rank, world, port, case, out_dir, transport="host"):
     aborts = ops.ws_aborts(reset=True)
     if aborts:
         raise RuntimeError(f"rank {rank}: {aborts} wave-specialised hand-off aborts")
+    if comm is not None:  # the communicator cannot be destroyed under a live executor
+        try:
+            comm.close()
+        except RuntimeError:
+            pass
+        else:
+            raise RuntimeError("RcclComm.close succeeded while a ShardStream still used it")
     sh.close()
     if comm is not None:
         comm.close()
+        if comm.handle:
+            raise RuntimeError("RcclComm.close left the handle set")
     np.save(os.path.join(out_dir, f"{case}_rank{rank}.npy"), np.stack(outs))
     if rank == 0:  # the whole stream as the GPU generates it, for the oracle
         full = _stream_piece(ops, torch, i8, 0, H + world * STEPS * L, dev)

@@ -18,7 +18,7 @@ import bench  # noqa: E402
 from gpusdr import ops  # noqa: E402
 from gpusdr._native import lib  # noqa: E402
 
-KINDS = ["planesFull", "planesFree", "partsFull", "partsFree", "pstat", "tapsRead", "amFull", "amFree"]
+KINDS = ["planesFull", "planesFree", "partsFull", "partsFree", "pstat", "tapsRead", "amSlot", "amFree"]
 SLOTS = 10
 
 

@@ -21,13 +21,14 @@ from gpusdr import chain as chain_mod  # noqa: E402
 from gpusdr import ops  # noqa: E402
 from gpusdr._native import HipError, lib  # noqa: E402
 
-NAMES = ["aborted_waits", "hist_oob", "ring_window_oob", "ring_write_oob", "hist_reads", "ring_reads"]
+NAMES = ["aborted_waits", "hist_oob", "ring_window_oob", "ring_write_oob", "hist_reads", "ring_reads", "audio_tiles",
+         "audio_batches"]
 
 
 def diag(reset=True):
     v = (ctypes.c_ulonglong * 8)()
     assert lib().gsdrAmdWsDiag(v, int(reset)) == 0
-    return dict(zip(NAMES, list(v)[:6]))
+    return dict(zip(NAMES, list(v)))
 
 
 def scenario(spin):
@@ -61,8 +62,43 @@ def scenario(spin):
     return failed, aborts
 
 
+def history_scenario(spin):
+    """r05: a steady resident step - its audio windows reach into the AM history
+    (amH > 0, the history branch) - under `spin`, after a first step at the normal limit."""
+    T, D, Ta, Da, L = 1023, 10, 255, 20, 1_000_000
+    rng = np.random.default_rng(23)
+    rf = orc.lowpass_taps(T, 0.04)
+    au = orc.lowpass_taps(Ta, 0.02)
+    dev = torch.from_numpy(rng.integers(-128, 128, size=2 * L * 4).astype(np.int8)).cuda()
+    ops.ws_aborts(reset=True)
+    c = chain_mod.AmChain(rf, D, au, Da, L)
+    out = torch.empty(4 * (L // (D * Da)), dtype=torch.float32, device="cuda")
+    c.step_resident(dev, 2, out)  # first step, normal limit
+    c.torch_stream.synchronize()
+    diag(True)
+    prev = ops.set_ws_spin_limit(spin)
+    failed = 0
+    try:
+        try:
+            c.step_resident(dev[2 * L * 2:], 2, out)  # steady: RF history in place, AM history amH > 0
+        except HipError:
+            failed += 1
+        c.torch_stream.synchronize()
+        aborts = ops.ws_aborts(reset=True)
+        c.close()
+    finally:
+        ops.set_ws_spin_limit(prev)
+        ops.ws_aborts(reset=True)
+    return failed, aborts
+
+
 if __name__ == "__main__":
     diag(True)
-    for spin in (0, 0, 1 << 22):
+    # the same launches at the normal limit first: their batch count is the model for the aborted runs
+    for spin in (1 << 22, 0, 0):
         failed, aborts = scenario(spin)
         print(f"spin limit {spin}: failed steps {failed}, abort count left {aborts}, diag {diag(True)}", flush=True)
+    for spin in (1 << 22, 0, 0):
+        failed, aborts = history_scenario(spin)
+        print(f"steady step (amH > 0), spin limit {spin}: failed {failed}, aborts {aborts}, diag {diag(True)}",
+              flush=True)

@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
-"""Build provenance: one sha256 over the sources libgpusdrpipeline.so is built from (the kernels, the
-runtime, the C API, the public headers and the Makefile), path by path in sorted order. The Makefile
-embeds it in the library (gsdrAmdBuildId); tests/test_abi_exports.py compares the two, so a stale
-pushed .so fails loudly instead of testing other code than the tree's.
-Usage: source_hash.py [repo root]   -> prints the 16-hex-digit id"""
+"""Build provenance: one sha256 over what libgpusdrpipeline.so is built from - the sources (the kernels,
+the runtime, the C API, the public headers and the Makefile, path by path in sorted order), the extra
+compile flags (EXTRA_FLAGS: the -D switches of A/B and diagnostic builds), the target architecture and
+the compiler's version string. The Makefile embeds it in the library (gsdrAmdBuildId);
+tests/test_abi_exports.py compares the two, so a stale pushed .so - or one built with a diagnostic or
+A/B define - fails loudly instead of testing other code than the tree's.
+Usage: source_hash.py [repo root] [--extra-flags FLAGS] [--arch ARCH] [--hipcc PATH]
+       -> prints the 16-hex-digit id"""
+import argparse
+import functools
 import hashlib
 import os
-import sys
+import subprocess
 
 SUFFIXES = (".hip", ".cpp", ".h", ".hpp")
+DEFAULT_HIPCC = "/opt/rocm/bin/hipcc"
+DEFAULT_ARCH = "gfx950"
 
 
 def source_files(root):
@@ -20,16 +27,36 @@ def source_files(root):
     return sorted(files, key=lambda p: os.path.relpath(p, root))
 
 
-def source_hash(root):
+@functools.lru_cache(maxsize=4)
+def compiler_version(hipcc=DEFAULT_HIPCC):
+    """The compiler's --version text (HIP and clang versions); '' where it cannot run."""
+    try:
+        r = subprocess.run([hipcc, "--version"], capture_output=True, text=True, timeout=60)
+        return r.stdout.strip()
+    except (OSError, subprocess.SubprocessError):
+        return ""
+
+
+def source_hash(root, extra_flags="", arch=DEFAULT_ARCH, hipcc=DEFAULT_HIPCC):
+    """The build id of a library built from `root` with EXTRA_FLAGS=extra_flags (the product build:
+    none) for `arch` by `hipcc`."""
     h = hashlib.sha256()
     for p in source_files(root):
         rel = os.path.relpath(p, root).replace(os.sep, "/")
         with open(p, "rb") as f:
             data = f.read()
         h.update(rel.encode() + b"\0" + str(len(data)).encode() + b"\0" + data)
+    for key, val in (("EXTRA_FLAGS", " ".join(extra_flags.split())), ("ARCH", arch),
+                     ("COMPILER", compiler_version(hipcc))):
+        h.update(b"\1" + key.encode() + b"=" + val.encode() + b"\0")
     return h.hexdigest()[:16]
 
 
 if __name__ == "__main__":
-    print(source_hash(os.path.abspath(sys.argv[1] if len(sys.argv) > 1 else
-                                      os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root", nargs="?", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    ap.add_argument("--extra-flags", default="")
+    ap.add_argument("--arch", default=DEFAULT_ARCH)
+    ap.add_argument("--hipcc", default=DEFAULT_HIPCC)
+    a = ap.parse_args()
+    print(source_hash(os.path.abspath(a.root), a.extra_flags, a.arch, a.hipcc))
