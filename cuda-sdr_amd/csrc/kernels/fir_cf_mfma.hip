@@ -1283,6 +1283,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
 #pragma unroll
     for (int j = 0; j < G; ++j) wsI8LoadGroup<G>(r1, Wl, ptid, j, wB);
     float ht[kAudioTapsPerLane];  // audio taps (lane % 8) + 8 u
+    AudioBounds ab = AUD ? audioBounds(a8, t0, n, lead) : AudioBounds{0, 0, 0};
 #pragma unroll
     for (int u = 0; u < kAudioTapsPerLane; ++u) {
       const int tp = (lane & 7) + 8 * u;
@@ -1290,16 +1291,16 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
     }
     for (int i = 0;; i += 2) {
       wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
-        if (AUD && i >= kAudioLag) wsAudioTile(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht);
+        if (AUD && i >= kAudioLag) wsAudioTile(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht, ab);
       });
       if (i + 1 >= n) break;
       wsI8ProducerTile<G>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
-        if (AUD && i + 1 >= kAudioLag) wsAudioTile(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht);
+        if (AUD && i + 1 >= kAudioLag) wsAudioTile(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht, ab);
       });
       if (i + 2 >= n) break;
     }
     if constexpr (AUD)
-      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile(a8, ring, c, t0, n, lead, t, ptid, ht);
+      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile(a8, ring, c, t0, n, lead, t, ptid, ht, ab);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if GSDR_WS_WAITS
     wsSpanStore(__builtin_amdgcn_s_memtime() - span0);
@@ -1517,6 +1518,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsGroupKernel(I8DecArgs a8
 #pragma unroll
     for (int j = 0; j < G; ++j) wsI8LoadGroup<G>(r1, Wl, ptid, j, wB);
     float ht[kAudioTapsPerLane];
+    AudioBounds ab = AUD ? audioBounds(a8, t0, n, lead) : AudioBounds{0, 0, 0};
 #pragma unroll
     for (int u = 0; u < kAudioTapsPerLane; ++u) {
       const int tp = (lane & 7) + 8 * u;
@@ -1524,16 +1526,16 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsGroupKernel(I8DecArgs a8
     }
     for (int i = 0;; i += 2) {
       wsI8ProducerTile<G, kGWaves>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
-        if (AUD && i >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht);
+        if (AUD && i >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht, ab);
       });
       if (i + 1 >= n) break;
       wsI8ProducerTile<G, kGWaves>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
-        if (AUD && i + 1 >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht);
+        if (AUD && i + 1 >= kAudioLag) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht, ab);
       });
       if (i + 2 >= n) break;
     }
     if constexpr (AUD)
-      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, t, ptid, ht);
+      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, t, ptid, ht, ab);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }
@@ -2089,6 +2091,7 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
   a.Wu = 60 * a.D + 16 * a.KS;
   const int Wl = std::min(a.Wu, (511 * a.D + a.T + 7) / 8);
   if (Wl > 4 * kWsPThreads) return hipErrorNotSupported;
+  if (!audioIndexFits(tiles, (int64_t)amH, (int64_t)aN, (int64_t)aD, (int64_t)aT)) return hipErrorNotSupported;
   // the layout search costs ~1 ms of host time: cached per (D, KS) like the other launchers' (an
   // uncached search per call starved the GPU between eager launches: 0.70 ms per C5 step); a small
   // map, so chains with different RF decimations / tap counts stepped alternately stay cached
@@ -2104,6 +2107,7 @@ hipError_t launchFirI8DecMfmaAudio(const int8_t* iq, const float* taps, size_t t
     layCache.emplace_back(key, l);
     return l;
   };
+  a.audioPerm = cachedAudioSlotPerm((int)aD);
   if ((policy & GSDR_POLICY_I8_WS8) == 0) {  // the 4-way split-K kernel (r05)
     I8DecArgs w = a;
     w.aTaps = aTaps;

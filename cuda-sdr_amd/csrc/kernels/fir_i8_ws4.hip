@@ -23,6 +23,9 @@
 
 #include "fir_launch.h"
 #include "kcommon.h"
+// the waits profile (-DGSDR_WS_WAITS=1) counts the consumer waves 0-3 only: the producers' counted
+// vmcnt waits must not see its global atomics
+#define GSDR_WS_WAIT_WAVES 4
 #include "ws_common.h"
 
 #include <gsdr/gsdr_amd.h>
@@ -30,6 +33,10 @@
 namespace gsdr_amd {
 
 constexpr int kW4Consumers = 4;                                    // one per SIMD
+#ifndef GSDR_W4_SETS
+#define GSDR_W4_SETS 2
+#endif
+constexpr int kW4Sets = GSDR_W4_SETS;  // plane sets: the producers fill tile i while tiles i - kW4Sets + 1 .. i - 1 wait
 constexpr int kW4Threads = (kW4Consumers + kWsProducers) * kWave;  // 512
 constexpr int kW4PartialBytes = kW4Consumers * 16 * kWave * 4;     // 16 KB per partial buffer
 constexpr int kW4MaxKS = 22;                                       // K <= 4 x 22 x 16 = 1408
@@ -39,43 +46,52 @@ constexpr int kW4MaxKS = 22;                                       // K <= 4 x 2
 #define GSDR_W4_PF 3
 #endif
 
-// Consumer wave `wave` reduces accumulator registers wave, wave + 4 (I) and wave + 8, wave + 12 (Q)
-// of block-local tile j over the 4 waves' partials (wave order), then the epilogue: the AM ring and
-// the audio hand-off (AUD), or the output store.
+// Phase stamps, harness builds only (-DGSDR_W4_STAMPS, tools/exp/run_w4_variants.sh): per wave of the first
+// 256 workgroups the s_memtime cycles of each phase, summed in registers and stored once at the end
+// (plain stores: no atomics beside the producers' counted vmcnt waits). Consumers: 0 planesFull wait,
+// 1 partsFull wait, 2 MFMA loop (with the previous tile's partial reads and sums), 3 the two signals after
+// it, 4 partsFree / tapsRead waits, 5 partials write + signal, 6 epilogue, 7 the last tile's reduction;
+// producers: 0 audio stage, 1 window (vmcnt) wait, 2 planesFree wait, 3 convert + plane writes + loads.
+#ifdef GSDR_W4_STAMPS
+static __device__ unsigned long long gW4Stamps[256 * 8 * 9];
+#define W4ST(k)                                              \
+  {                                                          \
+    const unsigned long long now__ = __builtin_amdgcn_s_memtime(); \
+    cst[k] += now__ - tlast;                                 \
+    tlast = now__;                                           \
+  }
+#else
+#define W4ST(k)
+#endif
+
+// Partial sums in LDS (two buffers of 16 KB, tile i in buffer i & 1): writer wave v stores for reducer
+// wave r = 0..3 one float4 per lane, {acc[r], acc[r + 4], acc[r + 8], acc[r + 12]} at float4 index
+// (v 4 + r) 64 + lane - 4 ds_write_b128 per lane instead of 16 ds_write_b32, and the reducer reads its
+// four values of one writer with one ds_read_b128 (lanes 16 B apart: conflict free both ways). Reducer
+// r finishes accumulator registers r, r + 4 (I, output rows r + 4 half and r + 8 + 4 half) and r + 8,
+// r + 12 (Q of the same outputs): yi = ((p0 + p1) + p2) + p3 in writer order.
+__device__ __forceinline__ const f4* w4Part(const float* part, int b, int v, int r, int lane) {
+  return reinterpret_cast<const f4*>(part + b * (kW4PartialBytes / 4)) + (v * 4 + r) * kWave + lane;
+}
+
+// The epilogue values of block-local tile j from its sums y = {yi0, yi1, yq0, yq1}: the two AM samples of
+// this lane (AUD: held for the ring, and stored when the caller asked for the AM samples), or the outputs
+// stored right away. Accumulator register i = wave + 4 h holds row (i & 3) + 8 (i >> 2) + 4 half of the
+// 32 x 32 tile.
 template <int EPI, bool AUD>
-__device__ __forceinline__ void w4Reduce(const I8DecArgs& a, const float* part, WsCtl* c, float outScale, int tile,
-                                         int j, int tid, float* ring, bool lead) {
+__device__ __forceinline__ void w4Outputs(const I8DecArgs& a, float outScale, int tile, int j, int tid, f4 y, bool lead,
+                                          float (&am)[2]) {
   const int lane = tid & (kWave - 1);
   const int wave = tid >> 6;
   const int half = lane >> 5, col = lane & 31;
-  const int b = j & 1;
-  wsWait(c, &c->partsFull[b], kW4Consumers * ((j >> 1) + 1));
-  const float* pb = part + b * (kW4PartialBytes / 4);
-  float yi[2] = {0.0f, 0.0f}, yq[2] = {0.0f, 0.0f};
-#pragma unroll
-  for (int v = 0; v < kW4Consumers; ++v)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      yi[h] += pb[(v * 16 + wave + 4 * h) * kWave + lane];
-      yq[h] += pb[(v * 16 + wave + 4 * h + 8) * kWave + lane];
-    }
-  wsSignal(&c->partsFree[b], lane);
-  // slot j mod kAmRing is free once the producers finished the audio outputs of tile j - kAmRing + 1
-  if (AUD && j - kAmRing + 2 > 0) wsWait(c, &c->amFree, kWsProducers * (j - kAmRing + 2));
+  const float yi[2] = {y.x, y.y}, yq[2] = {y.z, y.w};
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    // accumulator register i = wave + 4 h holds row (i & 3) + 8 (i >> 2) + 4 half of the 32 x 32 tile
     const int orow = wave + 8 * h + 4 * half;
     const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + col;
     if constexpr (AUD) {
       const float v = __builtin_amdgcn_sqrtf(fmaf(yi[h], yi[h], yq[h] * yq[h])) * outScale;
-      const int pos = (j & (kAmRing - 1)) * kCfTileOut + 32 * orow + col;
-#if GSDR_WS_DIAG
-      wsDiag(3, pos < 0 || pos >= kAmRing * kCfTileOut);
-#endif
-      const float rv = k < a.nOut ? v : 0.0f;
-      ring[pos] = rv;
-      if (pos < kAmRingMirror) ring[kAmRing * kCfTileOut + pos] = rv;
+      am[h] = k < a.nOut ? v : 0.0f;
       // the lead tile belongs to the previous block (computed here only for the audio windows)
       if (a.out != nullptr && k < a.nOut && !(lead && j == 0)) reinterpret_cast<float*>(a.out)[k] = v;
     } else if (k < a.nOut) {
@@ -85,12 +101,60 @@ __device__ __forceinline__ void w4Reduce(const I8DecArgs& a, const float* part, 
         reinterpret_cast<f2*>(a.out)[k] = f2{yi[h], yq[h]} * outScale;
     }
   }
-  if constexpr (AUD) wsSignal(&c->amSlot[j & (kAmRing - 1)], lane);
 }
 
-// The consumer waves: B fragments of this wave's K quarter in VGPRs for the whole launch, then per
-// tile 2 KS MFMAs, the partials into buffer i & 1, and the reduction of the previous tile (so no wave
-// waits for the slowest one before its next MFMAs).
+// AUD: tile j's AM samples of this lane into ring slot j mod kAmRing (and its mirror). The slot must be
+// free - the producers done with the audio of tile j - kAmRing + 1 - which the caller waits for.
+__device__ __forceinline__ void w4RingWrite(float* ring, int j, int tid, const float (&am)[2]) {
+  const int lane = tid & (kWave - 1);
+  const int wave = tid >> 6;
+  const int half = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int pos = (j & (kAmRing - 1)) * kCfTileOut + 32 * (wave + 8 * h + 4 * half) + col;
+#if GSDR_WS_DIAG
+    wsDiag(3, pos < 0 || pos >= kAmRing * kCfTileOut);
+#endif
+    ring[pos] = am[h];
+    if (pos < kAmRingMirror) ring[kAmRing * kCfTileOut + pos] = am[h];
+  }
+}
+
+__device__ __forceinline__ void w4AmFreeWait(WsCtl* c, int j) {  // ring slot of tile j reusable
+  if (j - kAmRing + 2 > 0) wsWait(c, &c->amFree, kWsProducers * (j - kAmRing + 2));
+}
+
+#ifndef GSDR_W4_LATESIG
+#define GSDR_W4_LATESIG 1  // A/B switch: outputs formed between the partial writes and their signal
+#endif
+#ifndef GSDR_W4_CPRIO
+#define GSDR_W4_CPRIO 1
+#endif
+#ifndef GSDR_W4_NOFENCE  // A/B: hand-offs ordered by the LDS queue alone (no lgkmcnt(0) before a signal)
+#define GSDR_W4_NOFENCE 0
+#endif
+#ifndef GSDR_W4_READY
+#define GSDR_W4_READY 1  // A/B switch of the one-round-trip readiness check below
+#endif
+// Up to four hand-off counters checked in ONE LDS round trip (the four loads issued together, one wait):
+// true when every counter has reached its target (the caller then skips the individual waits). A
+// consumer wave starts each tile waiting on planesFull, partsFull, amFree and partsFree - one after the
+// other that was four serial LDS round trips per tile, and they are almost always already satisfied.
+__device__ __forceinline__ bool w4Ready(WsCtl* c, const int* p0, int g0, const int* p1, int g1, const int* p2, int g2,
+                                        const int* p3, int g3) {
+  const int v0 = __hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int v1 = __hip_atomic_load(p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int v2 = __hip_atomic_load(p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int v3 = __hip_atomic_load(p3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return waveUniform(v0) >= g0 && waveUniform(v1) >= g1 && waveUniform(v2) >= g2 && waveUniform(v3) >= g3;
+}
+
+// The consumer waves: B fragments of this wave's K quarter in VGPRs for the whole launch, then per tile
+// 2 KS MFMAs with the previous tile's reduction folded in - its four partial reads issued and summed in
+// the gaps between this tile's MFMAs - and, for the fused chain, the AM ring writes of the tile before
+// that (r05 stamps: as separate phases the reduction, the partial writes and the epilogue took ~40 % of a
+// consumer wave's span beside 43 % for its MFMAs: with one consumer wave per SIMD nothing hid their LDS
+// round trips); then the partials of this tile, and the previous tile's outputs formed in registers.
 template <int KS, int EPI, bool AUD>
 __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* smem, float* part, WsCtl* c, int sh,
                                             int t0, int n, int tid, float* ring, bool lead) {
@@ -115,49 +179,145 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
   }
   // the tap staging area becomes the partial-sum area once every consumer wave has its fragments
   wsSignal(&c->tapsRead, lane);
+  // the consumer (MFMA) wave's issue priority over its SIMD's producer wave: r05 A/B at C5, 5 runs,
+  // 142.9-146.7 vs 144.3-149.6 us per launch (4 of 5 faster); the producers at priority 1 instead: 161.8
+  if (GSDR_W4_CPRIO > 0) __builtin_amdgcn_s_setprio(GSDR_W4_CPRIO);
 
   const int arow = lane & 15;
   const int comp = (lane >> 4) & 1;
   const int uRow = 4 * D * arow + half;
   const float outScale = ldexpf(1.0f / 127.0f, -sh);
+  float am[2] = {0.0f, 0.0f};  // AUD: AM samples of tile i - 2 (this lane's), written to the ring in tile i's loop
+#ifdef GSDR_W4_STAMPS
+  unsigned long long cst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+  const unsigned long long tspan = tlast;
+#endif
   for (int i = 0; i < n; ++i) {
-    const int set = i & 1;
-    wsWait(c, &c->planesFull[set], kWsProducers * ((i >> 1) + 1));
+    const int set = i % kW4Sets;
+    const bool red = i >= 1;           // tile i - 1's partials (all four waves': each wrote them before its tile i)
+    const int rb = (i - 1) & 1;
+    const bool ringW = AUD && i >= 2;  // tile i - 2's AM samples go to the ring in this loop
+    const int b = i & 1;               // this tile's partial buffer: free once tile i - 2 is reduced
+    const int gFull = kWsProducers * (i / kW4Sets + 1);
+    const int gParts = red ? kW4Consumers * (((i - 1) >> 1) + 1) : 0;
+    const int gAm = ringW && i - 2 - kAmRing + 2 > 0 ? kWsProducers * (i - 2 - kAmRing + 2) : 0;
+    // the partial buffer: free once tile i - 2 is reduced (before that: once the tap staging area is read)
+    int* const pFree = i >= 2 ? &c->partsFree[b] : &c->tapsRead;
+    const int gFree = i >= 2 ? kW4Consumers * (i >> 1) : kW4Consumers;
+    const bool ready = GSDR_W4_READY && w4Ready(c, &c->planesFull[set], gFull, &c->partsFull[rb], gParts, &c->amFree, gAm, pFree, gFree);
+    if (ready) {
+      if (GSDR_W4_NOFENCE) asm volatile("" ::: "memory");
+      else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    } else {
+      wsWait(c, &c->planesFull[set], gFull);
+      if (red) wsWait(c, &c->partsFull[rb], gParts);
+      if (ringW) w4AmFreeWait(c, i - 2);
+    }
+    W4ST(0)
+    W4ST(1)
     const int8_t* pI = smem + set * 2 * a.planeStride + comp * a.planeStride;
     v16f acc = v16f{};
     h8 xa[KS];
+    f4 pv[kW4Consumers];
+    f4 y = f4{0.0f, 0.0f, 0.0f, 0.0f};
     auto readA = [&](int s) {
       xa[s] = *reinterpret_cast<const h8*>(pI + 16 * cfPhys(uRow + 2 * (wave * KS + s), a.padShift));
     };
+    // (the partial reads are unconditional - no branch in the K loop; at i = 0 they read buffer 1,
+    // whatever it holds, and the sums are not used)
+    auto readP = [&](int v) { pv[v] = (GSDR_WS_ABL & 2) ? f4{acc[v], 0.0f, 0.0f, 0.0f} : *w4Part(part, rb, v, wave, lane); };
 #pragma unroll
     for (int s = 0; s < PF; ++s) readA(s);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       if (s + PF < KS) readA(s + PF);
+      if (s < kW4Consumers) readP(s);
+      if (s == 0 && ringW) w4RingWrite(ring, i - 2, tid, am);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bh[s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bl[s], acc, 0, 0, 0);
+      if (!(GSDR_WS_ABL & 1)) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bl[s], acc, 0, 0, 0);
+      } else {
+        asm volatile("" ::"v"(xa[s]));
+        acc[s & 15] += 1.0f;
+      }
       __builtin_amdgcn_sched_barrier(0);
+      if (s >= 2 && s - 2 < kW4Consumers) y += pv[s - 2];  // writer order: v = s - 2
     }
-    wsSignal(&c->planesFree[set], lane);  // this wave's A reads are complete
-    const int b = i & 1;
-    wsWait(c, &c->partsFree[b], kW4Consumers * (i >> 1));  // tile i - 2 reduced by every wave
-    if (i < 2) wsWait(c, &c->tapsRead, kW4Consumers);
-    float* pb = part + b * (kW4PartialBytes / 4);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) pb[(wave * 16 + k) * kWave + lane] = acc[k];
+    for (int v = 0; v < kW4Consumers; ++v) {  // shares the K loop did not reach (KS < 6)
+      if (v >= KS) readP(v);
+      if (v >= KS - 2) y += pv[v];
+    }
+    W4ST(2)
+    // one release for the three hand-offs (their LDS reads and writes were all waited for in the loop);
+    // fenced one by one, each signal waited out the previous one's LDS atomic
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    wsSignalNF(&c->planesFree[set], lane);         // this wave's A reads are complete
+    if (red) wsSignalNF(&c->partsFree[rb], lane);  // and its reads of tile i - 1's partials
+    if (ringW) wsSignalNF(&c->amSlot[(i - 2) & (kAmRing - 1)], lane);  // tile i - 2 is in the ring
+    W4ST(3)
+    if (!ready) wsWait(c, pFree, gFree);  // tile i - 2 reduced by every wave (almost always seen above)
+    W4ST(4)
+    f4* pb = reinterpret_cast<f4*>(part + b * (kW4PartialBytes / 4));
+#pragma unroll
+    for (int r = 0; r < kW4Consumers; ++r)
+      if (!(GSDR_WS_ABL & 2)) pb[(wave * 4 + r) * kWave + lane] = f4{acc[r], acc[r + 4], acc[r + 8], acc[r + 12]};
+      else asm volatile("" ::"v"(acc[r]), "v"(acc[r + 4]), "v"(acc[r + 8]), "v"(acc[r + 12]));
+#if GSDR_W4_LATESIG  // the previous tile's outputs while the partial writes land
+    if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am);
+    W4ST(6)
+    if (GSDR_W4_NOFENCE) {
+      asm volatile("" ::: "memory");
+      wsSignalNF(&c->partsFull[b], lane);
+    } else {
+      wsSignal(&c->partsFull[b], lane);
+    }
+    W4ST(5)
+#else
     wsSignal(&c->partsFull[b], lane);
-    if (i >= 1) w4Reduce<EPI, AUD>(a, part, c, outScale, t0 + i - 1, i - 1, tid, ring, lead);
+    W4ST(5)
+    if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am);
+    W4ST(6)
+#endif
   }
-  if (n >= 1) w4Reduce<EPI, AUD>(a, part, c, outScale, t0 + n - 1, n - 1, tid, ring, lead);
+  if constexpr (AUD) {  // tile n - 2 (pending) into the ring
+    if (n >= 2) {
+      w4AmFreeWait(c, n - 2);
+      w4RingWrite(ring, n - 2, tid, am);
+      wsSignal(&c->amSlot[(n - 2) & (kAmRing - 1)], lane);
+    }
+  }
+  if (n >= 1) {  // the last tile's reduction on its own
+    const int j = n - 1, rb = j & 1;
+    wsWait(c, &c->partsFull[rb], kW4Consumers * ((j >> 1) + 1));
+    f4 y = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int v = 0; v < kW4Consumers; ++v) y += *w4Part(part, rb, v, wave, lane);
+    wsSignal(&c->partsFree[rb], lane);
+    w4Outputs<EPI, AUD>(a, outScale, t0 + j, j, tid, y, lead, am);
+    if constexpr (AUD) {
+      w4AmFreeWait(c, j);
+      w4RingWrite(ring, j, tid, am);
+      wsSignal(&c->amSlot[j & (kAmRing - 1)], lane);
+    }
+    W4ST(7)
+  }
+#ifdef GSDR_W4_STAMPS
+  if ((int)blockIdx.x < 256 && lane == 0) {
+    for (int k = 0; k < 8; ++k) gW4Stamps[((int)blockIdx.x * 8 + wave) * 9 + k] = cst[k];
+    gW4Stamps[((int)blockIdx.x * 8 + wave) * 9 + 8] = __builtin_amdgcn_s_memtime() - tspan;
+  }
+#endif
 }
 
 template <int KS, int G, int EPI, bool AUD>
 __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, int Wl) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  float* part = reinterpret_cast<float*>(smem + 4 * a8.planeStride);
-  float* ring = AUD ? reinterpret_cast<float*>(smem + 4 * a8.planeStride + 2 * kW4PartialBytes) : nullptr;
+  float* part = reinterpret_cast<float*>(smem + 2 * kW4Sets * a8.planeStride);
+  float* ring = AUD ? reinterpret_cast<float*>(smem + 2 * kW4Sets * a8.planeStride + 2 * kW4PartialBytes) : nullptr;
   __shared__ WsCtl ctl;
   __shared__ float waveMax[kW4Consumers + kWsProducers];
   WsCtl* c = &ctl;
@@ -196,7 +356,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
     part[i] = h;
     hm = fmaxf(hm, fabsf(h));
   }
-  for (int i = tid; i < 4 * a8.planeStride / 16; i += kW4Threads) reinterpret_cast<uint4*>(smem)[i] = uint4{0, 0, 0, 0};
+  for (int i = tid; i < 2 * kW4Sets * a8.planeStride / 16; i += kW4Threads) reinterpret_cast<uint4*>(smem)[i] = uint4{0, 0, 0, 0};
   // the AM ring starts zeroed: an audio window reads 256 ring samples whatever the tap count (the ones
   // past its taps times zero, and 0 * NaN is NaN: r04's stale-LDS defect)
   if constexpr (AUD && GSDR_WS_RING_ZERO)
@@ -209,10 +369,16 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
 #pragma unroll
   for (int v = 1; v < kW4Consumers + kWsProducers; ++v) hMax = fmaxf(hMax, waveMax[v]);
   const int sh = hMax > 0.0f ? 14 - ilogbf(hMax) : 0;  // max |h 2^sh| in [2^14, 2^15)
+#if GSDR_WS_WAITS
+  const unsigned long long span0 = __builtin_amdgcn_s_memtime();
+#endif
 
   if (wave >= kW4Consumers) {
     // ================= producers (firI8WsKernel's, signalling 4 consumer waves) =================
     const int ptid = tid - kW4Consumers * kWave;
+#ifdef GSDR_W4_PPRIO  // A/B builds only: the producer wave's issue priority over its SIMD's consumer
+    __builtin_amdgcn_s_setprio(GSDR_W4_PPRIO);
+#endif
     I8WsWindow<G> wA, wB;
     const i4v r0 = wsI8TileRsrc(a8, t0, true);
 #pragma unroll
@@ -221,31 +387,72 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
 #pragma unroll
     for (int j = 0; j < G; ++j) wsI8LoadGroup<G>(r1, Wl, ptid, j, wB);
     float ht[kAudioTapsPerLane];  // audio taps (lane % 8) + 8 u
+    AudioBounds ab = AUD ? audioBounds(a8, t0, n, lead) : AudioBounds{0, 0, 0};
 #pragma unroll
     for (int u = 0; u < kAudioTapsPerLane; ++u) {
       const int tp = (lane & 7) + 8 * u;
       ht[u] = AUD && tp < a8.aT ? a8.aTaps[tp] : 0.0f;
     }
+#if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
+    unsigned long long st[4] = {0, 0, 0, 0};
+    unsigned long long* stp = st;
+#ifdef GSDR_W4_STAMPS
+    const unsigned long long tspanP = __builtin_amdgcn_s_memtime();
+#endif
+#else
+    unsigned long long* stp = nullptr;
+#endif
     for (int i = 0;; i += 2) {
-      wsI8ProducerTile<G, kW4Consumers>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
-        if (AUD && i >= kAudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht);
-      });
+      wsI8ProducerTile<G, kW4Consumers, kW4Sets>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
+        if (AUD && i >= kAudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht, ab);
+      }, stp);
       if (i + 1 >= n) break;
-      wsI8ProducerTile<G, kW4Consumers>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
-        if (AUD && i + 1 >= kAudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht);
-      });
+      wsI8ProducerTile<G, kW4Consumers, kW4Sets>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
+        if (AUD && i + 1 >= kAudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht, ab);
+      }, stp);
       if (i + 2 >= n) break;
     }
+    (void)stp;
     if constexpr (AUD)
       for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t)
-        wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, t, ptid, ht);
+        wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, t, ptid, ht, ab);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the wave
+#ifdef GSDR_W4_STAMPS
+    if ((int)blockIdx.x < 256 && lane == 0) {
+      for (int k = 0; k < 4; ++k) gW4Stamps[((int)blockIdx.x * 8 + wave) * 9 + k] = st[k];
+      gW4Stamps[((int)blockIdx.x * 8 + wave) * 9 + 8] = __builtin_amdgcn_s_memtime() - tspanP;
+    }
+#endif
+#if GSDR_WS_WAITS
+    wsSpanStore(__builtin_amdgcn_s_memtime() - span0);
+    {  // the producer phases into its slots 10-13 (plain stores after the final vmcnt(0))
+      const int wg = (int)blockIdx.x;
+      if (wg < 256 && lane == 0)
+        for (int k = 0; k < 3; ++k) gWsWaits[(wg * 12 + wave) * kWaitSlots + 10 + k] = st[k];
+      if (wg < 256 && lane == 0) gWsWaits[(wg * 12 + wave) * kWaitSlots + 9] = st[3];
+    }
+#endif
     return;
   }
   w4Consumers<KS, EPI, AUD>(a8, smem, part, c, sh, t0, n, tid, ring, lead);
+#if GSDR_WS_WAITS
+  wsSpanStore(__builtin_amdgcn_s_memtime() - span0);
+#endif
 }
 
 // ---- host side ---------------------------------------------------------------------------------
+
+uint32_t cachedAudioSlotPerm(int aD) {  // ~40 k permutations scored once per audio decimation
+  static std::mutex mu;
+  static std::vector<std::pair<int, uint32_t>> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const auto& [d, p] : cache)
+    if (d == aD) return p;
+  const uint32_t p = audioSlotPerm(aD);
+  if (cache.size() >= 16) cache.erase(cache.begin());
+  cache.emplace_back(aD, p);
+  return p;
+}
 
 namespace {
 
@@ -290,6 +497,10 @@ int w4PickKS(int ksteps) {
 }
 
 hipError_t launchW4Any(const I8DecArgs& a, int Wl, size_t lds, int grid, int epi, bool audio, hipStream_t stream) {
+#ifdef GSDR_W4_HARNESS  // variant builds of tools/exp/run_w4_variants.sh: C5's fused shape only
+  if (a.KS != 21 || !audio || (Wl + kWsPThreads - 1) / kWsPThreads != 3) return hipErrorNotSupported;
+  return launchW4G<21, 3, kEpiAm, true>(a, Wl, lds, grid, stream);
+#endif
   switch (a.KS) {
     case 2: return launchW4KS<2>(a, Wl, lds, grid, epi, audio, stream);
     case 4: return launchW4KS<4>(a, Wl, lds, grid, epi, audio, stream);
@@ -332,7 +543,7 @@ hipError_t launchFirI8Ws4(I8DecArgs a, int ksteps, int epi, bool audio, hipStrea
         found = true;
       }
     if (!found) {
-      lay = cfPlaneLayout(a.D, a.KS, a.Wu, 4, extra, kW4Consumers * a.KS);
+      lay = cfPlaneLayout(a.D, a.KS, a.Wu, 2 * kW4Sets, extra, kW4Consumers * a.KS);
       if (cache.size() >= 16) cache.erase(cache.begin());
       cache.emplace_back(key, lay);
     }
@@ -341,12 +552,24 @@ hipError_t launchFirI8Ws4(I8DecArgs a, int ksteps, int epi, bool audio, hipStrea
   a.padShift = lay.padShift;
   a.planeStride = lay.planeStride;
   a.dbp = 1;
-  const size_t lds = 4 * (size_t)a.planeStride + extra;
+#ifdef GSDR_W4_IDPERM  // A/B builds only: consecutive outputs in slot order
+  if (audio) a.audioPerm = 0x76543210u;
+#else
+  if (audio) a.audioPerm = cachedAudioSlotPerm(a.aD);
+#endif
+  const size_t lds = 2 * kW4Sets * (size_t)a.planeStride + extra;
   if (lds > (size_t)kCfDynLdsMax) return hipErrorNotSupported;
   const int grid = (int)(a.tiles < 256 ? a.tiles : 256);
   if (hipError_t e = wsPrepareLaunch(stream, a.spinLimit, a.abortOut); e != hipSuccess) return e;
   return launchW4Any(a, Wl, lds, grid, epi, audio, stream);
 }
+
+#ifdef GSDR_W4_HARNESS
+// tools/exp/run_w4_variants.sh: this variant build's entry point (-DGSDR_W4_HARNESS=<name>)
+extern "C" hipError_t GSDR_W4_HARNESS(const void* args, int ksteps, hipStream_t stream) {
+  return launchFirI8Ws4(*static_cast<const I8DecArgs*>(args), ksteps, kEpiAm, true, stream);
+}
+#endif
 
 #if GSDR_WS_DIAG
 // this translation unit's counters (ws_common.h keeps one copy per unit), added to fir_cf_mfma.hip's
@@ -359,6 +582,27 @@ hipError_t w4DiagRead(unsigned long long* out8, int reset) {
     const unsigned long long z[8] = {};
     e = hipMemcpyToSymbol(HIP_SYMBOL(gWsDiag), z, sizeof z);
   }
+  return e;
+}
+#endif
+#if defined(GSDR_W4_HARNESS_STAMPS) && defined(GSDR_W4_STAMPS)
+extern "C" hipError_t GSDR_W4_HARNESS_STAMPS(unsigned long long* out, size_t n, int reset) {
+  hipError_t e = hipDeviceSynchronize();
+  const size_t m = n < (size_t)256 * 8 * 9 ? n : (size_t)256 * 8 * 9;
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(gW4Stamps), m * sizeof(unsigned long long));
+  if (e == hipSuccess && reset) {
+    void* p = nullptr;
+    e = hipGetSymbolAddress(&p, HIP_SYMBOL(gW4Stamps));
+    if (e == hipSuccess) e = hipMemset(p, 0, sizeof(unsigned long long) * 256 * 8 * 9);
+  }
+  return e;
+}
+#endif
+#if defined(GSDR_W4_HARNESS_WAITS) && GSDR_WS_WAITS
+hipError_t w4WaitsRead(unsigned long long* out, size_t n, int reset);
+extern "C" hipError_t GSDR_W4_HARNESS_WAITS(unsigned long long* out, size_t n, int reset) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = w4WaitsRead(out, n, reset);
   return e;
 }
 #endif

@@ -42,7 +42,10 @@ constexpr int kWsSpinLimit = 1 << 22;                       // default s_sleep(1
 // Fused audio stage (firI8WsKernel<.., AUD>): AM ring of kAmRing tiles in LDS; the producers compute
 // the audio outputs of tile i - kAudioLag after producing the planes of tile i.
 constexpr int kAmRing = 8;
-constexpr int kAudioLag = 5;
+#ifndef GSDR_AUDIO_LAG
+#define GSDR_AUDIO_LAG 5
+#endif
+constexpr int kAudioLag = GSDR_AUDIO_LAG;
 constexpr int kAmRingMirror = 256;  // ring[4096 + i] = ring[i] for i < 256: no wrap inside a window
 constexpr int kAudioMaxTaps = 256;  // 8 tap groups of 32 per output slot
 constexpr int kGWaves = 4;          // two-group kernel: consumer waves per group
@@ -72,15 +75,15 @@ constexpr int kGWaves = 4;          // two-group kernel: consumer waves per grou
 #define GSDR_WS_PF 3
 #endif
 struct WsCtl {
-  int planesFull[2];
-  int planesFree[2];
+  int planesFull[3];  // per plane set (the 8-way kernels use two, the 4-way kernel kW4Sets)
+  int planesFree[3];
   int partsFull[2];                   // per partial buffer (one buffer: index 0)
   int partsFree[2];
   int pstat;
   int tapsRead;                       // consumer waves done reading the taps staged in `part`
   int amFree;                         // producer waves done with the audio outputs of a tile
   int abort;
-  int mode[2];                        // per plane set: scale exponent sx, or kWsDirect
+  int mode[3];                        // per plane set: scale exponent sx, or kWsDirect
   float stat[2][2][kWsProducers];     // [tile parity][max, smallest block max][producer wave]
   int amSlot[kAmRing];                // fused audio stage: consumer waves' AM signals per ring slot
   // set once by thread 0 (not part of the zeroed hand-off words above)
@@ -110,6 +113,10 @@ __device__ __forceinline__ void wsSignal(int* p, int lane) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS writes/reads complete
   if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// A signal after the caller's own release fence (several hand-offs released by one fence)
+__device__ __forceinline__ void wsSignalNF(int* p, int lane) {
+  if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // Hand-off wait profile, diagnostic builds only (-DGSDR_WS_WAITS=1; the product build has none): per
 // wave of the first 256 workgroups, the shader cycles spent in each kind of wait (the WsCtl counter
@@ -117,7 +124,10 @@ __device__ __forceinline__ void wsSignal(int* p, int lane) {
 // Kinds: 0 planesFull, 1 planesFree, 2 partsFull, 3 partsFree, 4 pstat, 5 tapsRead, 6 amSlot (the
 // audio stage's per-ring-slot counts), 7 amFree; slot 8 = the wave's span, 9 = its wait count.
 #if GSDR_WS_WAITS
-constexpr int kWaitSlots = 10;
+#ifndef GSDR_WS_WAIT_WAVES  // the consumer waves (waves below it); the 4-way kernel's unit sets 4
+#define GSDR_WS_WAIT_WAVES kCfWaves
+#endif
+constexpr int kWaitSlots = 13;  // + the 4-way consumers' phases: 10 MFMA loop, 11 partials write, 12 reduce
 static __device__ unsigned long long gWsWaits[256 * 12 * kWaitSlots];
 __device__ __forceinline__ int wsWaitKind(const WsCtl* c, const int* p) {
   const int off = (int)(reinterpret_cast<const char*>(p) - reinterpret_cast<const char*>(c));  // byte offset
@@ -136,7 +146,7 @@ __device__ __forceinline__ int wsWaitKind(const WsCtl* c, const int* p) {
 // span once, after their final vmcnt(0).
 __device__ __forceinline__ void wsWaitAdd(WsCtl*, int slot, unsigned long long v) {
   const int wg = (int)blockIdx.x, w = (int)(threadIdx.x >> 6);
-  if (wg < 256 && w < kCfWaves && (threadIdx.x & 63) == 0) atomicAdd(&gWsWaits[(wg * 12 + w) * kWaitSlots + slot], v);
+  if (wg < 256 && w < GSDR_WS_WAIT_WAVES && (threadIdx.x & 63) == 0) atomicAdd(&gWsWaits[(wg * 12 + w) * kWaitSlots + slot], v);
 }
 __device__ __forceinline__ void wsSpanStore(unsigned long long v) {
   const int wg = (int)blockIdx.x, w = (int)(threadIdx.x >> 6);
@@ -195,6 +205,19 @@ __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
 #endif
 }
 
+// wsWait that also reports an abort, read in the same LDS round trip as the counter's first poll (the
+// fused audio stage stops on an abort; a separate read of the abort word cost it a round trip per tile)
+__device__ __forceinline__ bool wsWaitAb(WsCtl* c, int* p, int target) {
+  const int v0 = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int ab0 = __hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (waveUniform(v0) >= target) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    return waveUniform(ab0) != 0;
+  }
+  wsWait(c, p, target);
+  return waveUniform(__hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+}
+
 typedef int i4v __attribute__((ext_vector_type(4)));
 
 struct I8DecArgs {
@@ -227,10 +250,18 @@ struct I8DecArgs {
   int32_t kneed;     // K-steps of 16 that meet nonzero taps
   int32_t tcLen;     // f16 elements per tap copy
   int32_t tcStride;  // bytes between two tap-copy arrays (hi / lo limb of each shift)
+  // fused audio stage: output slot o of a wave's batch of 8 consecutive outputs takes output
+  // jb + ((audioPerm >> 4 o) & 7) (audioSlotPerm: the order that spreads the slots' ds_read_b32 over
+  // the LDS banks for this aD)
+  uint32_t audioPerm;
 };
 
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+#ifndef GSDR_WS_ABL  // timing ablations of the 4-way kernel (tools/exp/run_w4_variants.sh; outputs wrong):
+#define GSDR_WS_ABL 0  // 1 no MFMAs, 2 no partial exchange, 4 no plane writes
+#endif
 
 template <int G>
 struct I8WsWindow {
@@ -278,14 +309,30 @@ struct NoPre {
   __device__ void operator()() const {}
 };
 
-template <int G, int NC = kCfWaves, typename Pre = NoPre>
+// `st` (GSDR_WS_WAITS builds, 4-way kernel): per-producer-wave cycle sums [0] audio stage, [1] window
+// (vmcnt) wait, [2] planesFree wait, [3] the rest (convert, plane writes, load issue); nullptr: none.
+// NS plane sets: tile i goes to set i % NS once the consumers are done with tile i - NS.
+template <int G, int NC = kCfWaves, int NS = 2, typename Pre = NoPre>
 __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
-                                                 int i, int ptid, I8WsWindow<G>& wCur, const Pre& pre = Pre{}) {
+                                                 int i, int ptid, I8WsWindow<G>& wCur, const Pre& pre = Pre{},
+                                                 unsigned long long* st = nullptr) {
   const int lane = ptid & (kWave - 1);
-  const int set = i & 1;
+  const int set = i % NS;
+#if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
+  unsigned long long t0s = __builtin_amdgcn_s_memtime(), t1s;
+#endif
   pre();
+#if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
+  if (st) { t1s = __builtin_amdgcn_s_memtime(); st[0] += t1s - t0s; t0s = t1s; }
+#endif
   wsI8WaitWindow<2 * G>(wCur);
-  wsWait(c, &c->planesFree[set], NC * (i >> 1));
+#if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
+  if (st) { t1s = __builtin_amdgcn_s_memtime(); st[1] += t1s - t0s; t0s = t1s; }
+#endif
+  wsWait(c, &c->planesFree[set], NC * (i / NS));
+#if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
+  if (st) { t1s = __builtin_amdgcn_s_memtime(); st[2] += t1s - t0s; t0s = t1s; }
+#endif
   int8_t* planes = smem + set * 2 * a.planeStride;
   const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
 #pragma unroll
@@ -298,38 +345,73 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
     uint4 iu, qu;
     int8IqToF16Units(words, iu, qu);
     const int off = 16 * cfPhys(g < Wl ? g : a.Wu, a.padShift);  // spare unit Wu: never read
-    *reinterpret_cast<uint4*>(planes + off) = iu;
-    *reinterpret_cast<uint4*>(planes + a.planeStride + off) = qu;
+    if (!(GSDR_WS_ABL & 4)) {
+      *reinterpret_cast<uint4*>(planes + off) = iu;
+      *reinterpret_cast<uint4*>(planes + a.planeStride + off) = qu;
+    } else {
+      asm volatile("" ::"v"(iu.x), "v"(iu.y), "v"(iu.z), "v"(iu.w), "v"(qu.x), "v"(qu.y), "v"(qu.z), "v"(qu.w));
+    }
     wsI8LoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
   }
   if (ptid == 0) c->mode[set] = 0;
   wsSignal(&c->planesFull[set], lane);
+#if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
+  if (st) st[3] += __builtin_amdgcn_s_memtime() - t0s;
+#endif
 }
 
 
 // Fused audio stage, producer side: the audio outputs of block-local tile t (global tile t0 + t) -
 // those whose window ends in that tile's AM range (tile 0 of the launch: also windows ending
 // before AM sample 0, in the history) - from the AM ring the consumers fill (tiles t - 1 and t are
-// in it: a window spans at most 256 AM samples), then amFree. A wave takes 8 outputs at a time,
-// jb + 4 o (o < 8, wave pw from jb = jLo + pw): lane l works on slot o = l / 8 with the taps
-// q + 8 u of its tap group q = l % 8 (u < 32; 32 LDS reads and FMAs, the 8 lanes of a slot reading
-// consecutive AM samples), then the slot's 8 partial sums meet in 3 DPP adds - no LDS round trip
+// in it: a window spans at most 256 AM samples), then amFree. A wave takes 8 consecutive outputs at a
+// time, jb + perm(o) (o < 8, wave pw from jb = jLo + 8 pw): lane l works on slot o = l / 8 with the
+// taps q + 8 u of its tap group q = l % 8 (u < 32; 32 LDS reads and FMAs, the 8 lanes of a slot
+// reading consecutive AM samples), then the slot's 8 partial sums meet in 3 DPP adds - no LDS round trip
 // (a 64-lane sum per output through ds_bpermute serialised ~50 LDS round trips per tile and made the
 // producers, who feed the matrix cores, the bottleneck: C5 0.18 -> 0.71 ms per step).
 // The lead tile (the previous block's last, computed for the ring only) has no outputs here.
 constexpr int kAudioTapsPerLane = kAudioMaxTaps / 8;
+#ifndef GSDR_AUDIO_ROTATE
+#define GSDR_AUDIO_ROTATE 1
+#endif
+#ifndef GSDR_AUDIO_SKIP  // timing experiments only: the audio windows not computed (outputs wrong)
+#define GSDR_AUDIO_SKIP 0
+#endif
 
 
-// smallest audio output j whose window end j aD - amH + aT - 1 is >= X (AM index X of this launch)
-__device__ __forceinline__ int64_t audioFirstJ(const I8DecArgs& a, int64_t X) {
-  const int64_t num = X + a.amH - a.aT + 1;
-  return num <= 0 ? 0 : (num + a.aD - 1) / a.aD;
+// smallest audio output j whose window end j aD - amH + aT - 1 is >= X (AM index X of this launch). In
+// 32 bits: the launcher admits only launches whose AM indices, history and audio offsets stay below 2^31
+// (audioIndexFits). r05: the 64-bit divisions here (four per tile and producer wave, a software sequence
+// of ~100 instructions each) were most of the producers' audio-stage time.
+__device__ __forceinline__ int audioFirstJ(const I8DecArgs& a, int X) {
+  const int num = X + a.amH - a.aT + 1;
+  return num <= 0 ? 0 : (int)((uint32_t)(num + a.aD - 1) / (uint32_t)a.aD);
 }
 
-// t0 / n: the block's tile range (lead included); t: the block-local tile whose audio outputs to compute.
+// The audio outputs a block owns (those whose window ends in its own tiles, the lead excluded, below aN),
+// from the launch's shape alone; `next`: the first output of the next tile the stage processes (tiles are
+// processed in order, and a tile's outputs end where the next one's begin - one division per tile).
+struct AudioBounds {
+  int lo, hi, next;
+  int batches;  // 8-output batches dealt so far: the next tile's first batch goes to wave batches % 4
+};
+__device__ __forceinline__ AudioBounds audioBounds(const I8DecArgs& a, int t0, int n, bool lead) {
+  const int own0 = t0 + (lead ? 1 : 0);
+  AudioBounds b;
+  b.lo = own0 == 0 ? 0 : audioFirstJ(a, own0 * kCfTileOut);
+  b.hi = audioFirstJ(a, (t0 + n) * kCfTileOut);
+  if (b.hi > (int)a.aN) b.hi = (int)a.aN;
+  b.next = b.lo;
+  b.batches = 0;
+  return b;
+}
+
+// t0 / n: the block's tile range (lead included); t: the block-local tile whose audio outputs to compute
+// (called for t = 0, 1, ... in order); ab: audioBounds of the block.
 template <int NSIG = kCfWaves>
 __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* ring, WsCtl* c, int t0, int n, bool lead,
-                                            int t, int ptid, const float (&ht)[kAudioTapsPerLane]) {
+                                            int t, int ptid, const float (&ht)[kAudioTapsPerLane], AudioBounds& ab) {
   const int lane = ptid & (kWave - 1);
   const int pw = ptid >> 6;
   const int o = lane >> 3, q = lane & 7;
@@ -347,37 +429,43 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
     // test_am_chain_device_steps at T = 127 / D = 1 and T = 64 / D = 3.)
     // Tile t - 1's slot was waited for by this wave's previous call (audio tiles run in order),
     // except when that call was the lead tile's, which has no outputs and waits for nothing.
-    wsWait(c, &c->amSlot[t & (kAmRing - 1)], NSIG * (t / kAmRing + 1));
-    if (lead && t == 1) wsWait(c, &c->amSlot[0], NSIG);
     // an aborted launch computes nothing more: its outputs are undefined anyway (the next call fails),
     // and no window is formed from ring slots a finished pipeline would not hold
-    const bool aborted = waveUniform(__hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+    bool aborted = wsWaitAb(c, &c->amSlot[t & (kAmRing - 1)], NSIG * (t / kAmRing + 1));
+    if (lead && t == 1) aborted |= wsWaitAb(c, &c->amSlot[0], NSIG);
 #if GSDR_WS_DIAG
     wsDiag(0, lane == 0 && aborted);
 #endif
-    const int64_t g = (int64_t)(t0 + t);
+    const int g = t0 + t;
     // the tile's outputs, clamped to the block's own range (its tiles after the lead) and to aN: the
     // loop bounds follow from the launch's shape alone, whatever a wait returned
-    const int64_t own0 = (int64_t)t0 + (lead ? 1 : 0);
-    const int64_t jBlkLo = own0 == 0 ? 0 : audioFirstJ(a, own0 * kCfTileOut);
-    int64_t jBlkHi = audioFirstJ(a, ((int64_t)t0 + n) * kCfTileOut);
-    if (jBlkHi > a.aN) jBlkHi = a.aN;
-    int64_t jLo = g == 0 ? 0 : audioFirstJ(a, g * kCfTileOut);
-    int64_t jHi = audioFirstJ(a, (g + 1) * kCfTileOut);
-    jLo = jLo > jBlkLo ? jLo : jBlkLo;
-    jHi = jHi < jBlkHi ? jHi : jBlkHi;
-    if (aborted) jHi = jLo;
-    for (int64_t jb = jLo + pw; jb < jHi; jb += 8 * kWsProducers) {
+    const int jLo = ab.next;
+    int jHi = audioFirstJ(a, (g + 1) * kCfTileOut);
+    jHi = jHi < ab.hi ? jHi : ab.hi;
+    jHi = jHi > jLo ? jHi : jLo;
+    ab.next = jHi;
+    // batches dealt round robin over the whole block, not from wave 0 at every tile: at aD = 20 a tile
+    // has 51-52 outputs = 7 batches, and waves 0-2 took two each tile while wave 3 took one - the
+    // planes hand-off waits for the slowest producer wave
+    const int first = GSDR_AUDIO_ROTATE ? (ab.batches & (kWsProducers - 1)) : 0;
+    ab.batches += (jHi - jLo + 7) >> 3;
+    const int pwr = (pw - first) & (kWsProducers - 1);
+    if (aborted || GSDR_AUDIO_SKIP) jHi = jLo;
+    // r05: 8 consecutive outputs per wave batch, slots ordered by audioPerm. Through r04 a batch took
+    // outputs jb + 4 o: at aD = 20 the windows of slots o and o + 2 then started 160 floats apart, on the
+    // same LDS banks - every audio ds_read_b32 2-way conflicted (6.6 M of the C5 launch's 37 M LDS cycles)
+    const int perm = (int)((a.audioPerm >> (4 * o)) & 7u);
+    for (int jb = jLo + 8 * pwr; jb < jHi; jb += 8 * kWsProducers) {
 #if GSDR_WS_DIAG
       wsDiag(7, lane == 0);
 #endif
-      const int64_t j = jb + kWsProducers * o;
-      const int64_t k0 = j * a.aD - a.amH;  // this slot's window: AM samples k0 .. k0 + aT - 1
+      const int j = jb + perm;
+      const int k0 = j * a.aD - a.amH;  // this slot's window: AM samples k0 .. k0 + aT - 1
       float s = 0.0f;
       if (jb * a.aD - a.amH >= 0) {  // wave-uniform: every window of the batch lies in the ring
         // block-local AM index, wrapped once: the mirror behind the ring keeps the window contiguous
         // (immediate-offset LDS reads)
-        const float* w = ring + (((int)(k0 - (int64_t)kCfTileOut * t0) + q) & (kAmRing * kCfTileOut - 1));
+        const float* w = ring + ((k0 - kCfTileOut * t0 + q) & (kAmRing * kCfTileOut - 1));
 #if GSDR_WS_DIAG
         if (j < jHi) {
           const int64_t kk0 = k0 - (int64_t)kCfTileOut * t0 + q, kk1 = kk0 + 8 * (kAudioTapsPerLane - 1);
@@ -385,8 +473,17 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
           wsDiag(5, true);
         }
 #endif
+        // all 32 reads in flight before the first FMA, then four interleaved partial sums (r05: the
+        // compiler had paired the reads into 16 ds_read2_b32, each waited for in full (lgkmcnt(0))
+        // before its two FMAs - 16 serialised LDS round trips per batch, ~half of the producers' span)
+        float x[kAudioTapsPerLane];
 #pragma unroll
-        for (int u = 0; u < kAudioTapsPerLane; ++u) s = fmaf(ht[u], w[8 * u], s);
+        for (int u = 0; u < kAudioTapsPerLane; ++u) x[u] = w[8 * u];
+        asm volatile("" ::: "memory");
+        float p4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int u = 0; u < kAudioTapsPerLane; ++u) p4[u & 3] = fmaf(ht[u], x[u], p4[u & 3]);
+        s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
       } else {  // windows reaching into the history (the launch's first outputs)
         // buffer loads (range-checked): a pointer select between the ring and the history would
         // compile to FLAT loads
@@ -394,7 +491,7 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
                                                           0x00020000);
 #pragma unroll 4
         for (int u = 0; u < kAudioTapsPerLane; ++u) {
-          const int64_t k = k0 + q + 8 * u;
+          const int k = k0 + q + 8 * u;
           float x;
 #if GSDR_WS_DIAG
           if (j < jHi) {
@@ -405,7 +502,7 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
           }
 #endif
           if (k >= 0)
-            x = ring[(int)(k - (int64_t)kCfTileOut * t0) & (kAmRing * kCfTileOut - 1)];
+            x = ring[(k - kCfTileOut * t0) & (kAmRing * kCfTileOut - 1)];
           else
             x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * (a.amH + k)), 0, 0));
           s = fmaf(ht[u], x, s);
@@ -478,6 +575,60 @@ inline CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes, size_t extra =
 }
 
 
+// The fused audio stage computes AM / audio indices in 32 bits: every AM index of the launch (tiles x 512
+// plus the history) and every audio window offset (j aD, j <= aN + 8) must stay below 2^31.
+inline bool audioIndexFits(int64_t tiles, int64_t amH, int64_t aN, int64_t aD, int64_t aT) {
+  const int64_t lim = (int64_t)1 << 30;  // headroom for the sums formed on top of each
+  return tiles * 512 + 512 + amH + aT < lim && (aN + 16) * aD + amH < lim;
+}
+
+// The order of the 8 output slots of an audio batch (8 consecutive outputs, aD samples apart): the
+// permutation whose two 32-lane halves (slots 0-3, 4-7; each slot's 8 lanes read 8 consecutive floats)
+// hit the fewest distinct addresses per LDS bank in a ds_read_b32 (2 groups of 32 lanes, 32 banks).
+// At aD = 20: outputs 0, 2, 4, 6 | 1, 3, 5, 7 - conflict free. Packed 4 bits per slot.
+inline uint32_t audioSlotPerm(int aD) {
+  int perm[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+  int best[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+  int bestCost = 1 << 30;
+  auto cost = [&](const int* p) {
+    int c = 0;
+    for (int h = 0; h < 2; ++h) {
+      int hits[32] = {};
+      int worst = 0;
+      for (int o = 4 * h; o < 4 * h + 4; ++o)
+        for (int q = 0; q < 8; ++q) {
+          const int bank = (int)(((int64_t)p[o] * aD + q) & 31);
+          worst = ++hits[bank] > worst ? hits[bank] : worst;
+        }
+      c += worst;
+    }
+    return c;
+  };
+  // all 8! orders; the first of the cheapest (the identity when nothing beats it)
+  auto visit = [&](auto&& self, int k) -> void {
+    if (k == 8) {
+      const int c = cost(perm);
+      if (c < bestCost) {
+        bestCost = c;
+        for (int i = 0; i < 8; ++i) best[i] = perm[i];
+      }
+      return;
+    }
+    for (int i = k; i < 8; ++i) {
+      const int t = perm[k];
+      perm[k] = perm[i];
+      perm[i] = t;
+      self(self, k + 1);
+      perm[i] = perm[k];
+      perm[k] = t;
+    }
+  };
+  visit(visit, 0);
+  uint32_t packed = 0;
+  for (int o = 0; o < 8; ++o) packed |= (uint32_t)best[o] << (4 * o);
+  return packed;
+}
+
 // Before a wave-specialised launch: report an earlier launch's abort (hipErrorLaunchTimeOut), arm this
 // one (spin limit, the device's abort word). Defined in fir_cf_mfma.hip.
 hipError_t wsPrepareLaunch(hipStream_t stream, int32_t& spinLimit, uint32_t*& abortOut);
@@ -486,5 +637,7 @@ hipError_t wsPrepareLaunch(hipStream_t stream, int32_t& spinLimit, uint32_t*& ab
 // nOut / nIn / tiles (and, with `audio`, the audio fields) are set: hipErrorNotSupported when the
 // shape does not fit it.
 hipError_t launchFirI8Ws4(I8DecArgs a, int ksteps, int epi, bool audio, hipStream_t stream);
+// audioSlotPerm(aD), cached (fir_i8_ws4.hip)
+uint32_t cachedAudioSlotPerm(int aD);
 
 }  // namespace gsdr_amd

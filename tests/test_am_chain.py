@@ -254,30 +254,31 @@ def test_am_chain_reports_ws_abort(chain_mod, orc):
 def test_am_chain_resident_rejects_pointer_without_history(chain_mod, orc):
     """A non-first resident step reads its RF history in place, 2 r bytes in front of its input (the
     documented contract). r04's diagnostic script broke it once and faulted the GPU (illegal memory
-    access); the step now checks the input's allocation and returns hipErrorInvalidValue when the history
-    in front, or the chunks after, would fall outside it - with no launch."""
+    access); the step now checks the input's device allocation (hipMemGetAddressRange) and returns
+    hipErrorInvalidValue - with no launch - when the history in front, or the chunks after, fall outside it."""
+    import ctypes
     import torch
-    from gpusdr._native import HipError
+    from gpusdr.chain import _L
     T, D, Ta, Da, L = 1023, 10, 255, 20, 100_000
     rf = orc.lowpass_taps(T, 0.04)
     au = orc.lowpass_taps(Ta, 0.02)
     c = chain_mod.AmChain(rf, D, au, Da, L)
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()  # the next allocation starts its own device allocation
-    raw = torch.zeros(2 * L * 3 + 3 * 2**20 + 2, dtype=torch.int8, device="cuda")
+    raw = torch.zeros(2 * L * 3, dtype=torch.int8, device="cuda")
     out = torch.empty(c.resident_output_count(2) + 16, dtype=torch.float32, device="cuda")
-    import ctypes
-    from gpusdr.chain import _L
+    # the allocation that holds raw (the caching allocator's segment: it may extend past the tensor)
+    hip = ctypes.CDLL("libamdhip64.so")
+    base, size = ctypes.c_void_p(), ctypes.c_size_t()
+    assert hip.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), ctypes.c_void_p(raw.data_ptr())) == 0
+    lo, hi = base.value, base.value + size.value
     got = ctypes.c_size_t()
-    # through the C ABI (the Python wrapper already refuses a short view): 2 chunks from a pointer one
-    # chunk before the allocation's end
-    r = _L().gsdrAmChainStepResident(c._h, raw.data_ptr() + raw.numel() - 2 * L, 2, out.data_ptr(), ctypes.byref(got))
-    assert r != 0
+    # through the C ABI (the Python wrapper refuses short views itself): 2 chunks from one chunk before the
+    # allocation's end
+    assert _L().gsdrAmChainStepResident(c._h, hi - 2 * L, 2, out.data_ptr(), ctypes.byref(got)) != 0
     n = c.step_resident(raw, 2, out)  # a valid first step
     assert n > 0
-    with pytest.raises(HipError):  # non-first step at the allocation's start: no room for its history
-        c.step_resident(raw[2:], 2, out)
-    m = c.step_resident(raw[2 * L * 2 - 2 * L:], 1, out)  # a valid continuation (history in front)
+    # a non-first step at the allocation's first byte: no room for its history in front
+    assert _L().gsdrAmChainStepResident(c._h, lo, 1, out.data_ptr(), ctypes.byref(got)) != 0
+    m = c.step_resident(raw[2 * L:], 1, out)  # a valid continuation (the history in front)
     torch.cuda.synchronize()
     assert m > 0
     c.close()

@@ -19,7 +19,7 @@ from gpusdr import ops  # noqa: E402
 from gpusdr._native import lib  # noqa: E402
 
 KINDS = ["planesFull", "planesFree", "partsFull", "partsFree", "pstat", "tapsRead", "amSlot", "amFree"]
-SLOTS = 10
+SLOTS = 13
 
 
 def waits(reset):
@@ -31,6 +31,10 @@ def waits(reset):
 
 if __name__ == "__main__":
     dev = torch.device("cuda", 0)
+    ws8 = "--ws8" in sys.argv  # the r04 8-way kernel (GSDR_POLICY_I8_WS8); default: the r05 4-way kernel
+    if ws8:
+        ops.set_kernel_policy(ops.POLICY_I8_WS8)
+    nc = 8 if ws8 else 4  # consumer waves per workgroup; the producers follow (4)
     chain = bench.AmChainSharded(ops, 0, 1, dev)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 1.0:
@@ -41,12 +45,22 @@ if __name__ == "__main__":
     chain.step()
     torch.cuda.synchronize()
     w = waits(True)
-    for role, sl in (("consumers (waves 0-7)", slice(0, 8)), ("producers (waves 8-11)", slice(8, 12))):
+    print(f"kernel: {'8-way (firI8WsKernel)' if ws8 else '4-way (firI8Ws4Kernel)'}")
+    for role, sl in ((f"consumers (waves 0-{nc - 1})", slice(0, nc)), (f"producers (waves {nc}-{nc + 3})", slice(nc, nc + 4))):
         x = w[:, sl, :]
         span = x[..., 8].sum()
         parts = ", ".join(f"{k} {x[..., i].sum() / span * 100:.1f}%" for i, k in enumerate(KINDS) if x[..., i].sum() > 0)
         print(f"{role}: median span {np.median(x[..., 8]):.0f} cycles, waits {x[..., 9].sum() / x[..., 9].size:.0f} "
               f"per wave; share of span waiting: {parts}; total {x[..., :8].sum() / span * 100:.1f}%", flush=True)
+        if not ws8 and sl.start == nc:  # the 4-way producers' phases (stamps)
+            print("  producer phases (share of span): " + ", ".join(
+                f"{k} {x[..., i].sum() / span * 100:.1f}%" for i, k in
+                ((10, "audio stage"), (11, "window vmcnt wait"), (12, "planesFree wait"), (9, "convert+writes+load issue"))),
+                flush=True)
+        if not ws8 and sl.start == 0:  # the 4-way consumers' phases (stamps)
+            print("  consumer phases (share of span): " + ", ".join(
+                f"{k} {x[..., i].sum() / span * 100:.1f}%" for i, k in
+                ((10, "MFMA loop"), (11, "partials write"), (12, "reduce+epilogue incl. its waits"))), flush=True)
     per_w = w[..., :8].sum(axis=2) / np.maximum(w[..., 8], 1)
     print("wait share by wave index (median over workgroups): " +
-          " ".join(f"w{i}:{np.median(per_w[:, i]) * 100:.0f}%" for i in range(12)))
+          " ".join(f"w{i}:{np.median(per_w[:, i]) * 100:.0f}%" for i in range(nc + 4)))
