@@ -144,4 +144,23 @@ __device__ __forceinline__ void int8IqToF16Units(const uint32_t (&w)[4], uint4& 
   qu = uint4{rq[0], rq[1], rq[2], rq[3]};
 }
 
+// The same four words -> the clamped samples as int8 I and Q halves-units (8 samples each, for the
+// int8 x int8 MFMA planes): x = -128 (0x80) becomes -127 (0x81), the reference's clamp. Per byte,
+// t = x ^ 0x80 is zero exactly for 0x80; (t - 1) & ~t & 0x80 flags it (the borrow can also flag a byte
+// t = 1, x = 0x81, above a flagged one - setting bit 0 of 0x81 changes nothing), and the flag shifted
+// to bit 0 turns 0x80 into 0x81.
+__device__ __forceinline__ uint32_t clampInt8x4(uint32_t x) {
+  const uint32_t t = x ^ 0x80808080u;
+  const uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;
+  return x | (z >> 7);
+}
+__device__ __forceinline__ void int8IqToI8Units(const uint32_t (&w)[4], uint2& iu, uint2& qu) {
+  uint32_t c[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c[q] = clampInt8x4(w[q]);
+  // bytes I0 Q0 I1 Q1 | I2 Q2 I3 Q3 of two words -> I0 I1 I2 I3 and Q0 Q1 Q2 Q3
+  iu = uint2{__builtin_amdgcn_perm(c[1], c[0], 0x06040200u), __builtin_amdgcn_perm(c[3], c[2], 0x06040200u)};
+  qu = uint2{__builtin_amdgcn_perm(c[1], c[0], 0x07050301u), __builtin_amdgcn_perm(c[3], c[2], 0x07050301u)};
+}
+
 }  // namespace gsdr_amd

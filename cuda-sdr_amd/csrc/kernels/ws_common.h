@@ -77,8 +77,8 @@ constexpr int kGWaves = 4;          // two-group kernel: consumer waves per grou
 struct WsCtl {
   int planesFull[3];  // per plane set (the 8-way kernels use two, the 4-way kernel kW4Sets)
   int planesFree[3];
-  int partsFull[2];                   // per partial buffer (one buffer: index 0)
-  int partsFree[2];
+  int partsFull[3];                   // per partial buffer (one buffer: index 0; the 4-way kernel has 3)
+  int partsFree[3];
   int pstat;
   int tapsRead;                       // consumer waves done reading the taps staged in `part`
   int amFree;                         // producer waves done with the audio outputs of a tile
@@ -92,7 +92,7 @@ struct WsCtl {
 };
 constexpr int kWsCtlZeroWords = (int)(offsetof(WsCtl, spinLimit) / 4);
 
-// Diagnostic builds only (-DGSDR_WS_DIAG=1, tools/gpu_r04_d.sh; the product build has none): bounds
+// Diagnostic builds only (-DGSDR_WS_DIAG=1: tools/build_variant.sh diag, run by tools/r05/session.sh diag; the product build has none): bounds
 // checks on every index the fused audio stage and the AM ring writes compute, counted per kind, to
 // show whether the abort path (a wsWait that returns early) computes an index outside its range -
 // [0] audio-tile waits that returned on an abort, [1] history index outside
@@ -260,7 +260,12 @@ struct I8DecArgs {
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
 #ifndef GSDR_WS_ABL  // timing ablations of the 4-way kernel (tools/exp/run_w4_variants.sh; outputs wrong):
-#define GSDR_WS_ABL 0  // 1 no MFMAs, 2 no partial exchange, 4 no plane writes
+#define GSDR_WS_ABL 0  // 1 no MFMAs, 2 no partial exchange, 4 no plane writes, 8 no int8 conversion
+#endif                 // (4-way Q8: 16 no partial exchange, 32 no A reads, 64 no MFMAs)
+#if 0
+#endif
+#ifndef GSDR_WS_MFREP  // timing experiments: each consumer MFMA pair issued MFREP times (outputs wrong)
+#define GSDR_WS_MFREP 1
 #endif
 
 template <int G>
@@ -311,8 +316,10 @@ struct NoPre {
 
 // `st` (GSDR_WS_WAITS builds, 4-way kernel): per-producer-wave cycle sums [0] audio stage, [1] window
 // (vmcnt) wait, [2] planesFree wait, [3] the rest (convert, plane writes, load issue); nullptr: none.
-// NS plane sets: tile i goes to set i % NS once the consumers are done with tile i - NS.
-template <int G, int NC = kCfWaves, int NS = 2, typename Pre = NoPre>
+// NS plane sets: tile i goes to set i % NS once the consumers are done with tile i - NS. Q8: int8 planes
+// (the 4-way kernel's int8 x int8 MFMA form): the 8 samples of a group are one 8-byte half of a 16-byte
+// plane slot, slot g / 2 (padded like the f16 units), half g % 2.
+template <int G, int NC = kCfWaves, int NS = 2, bool Q8 = false, typename Pre = NoPre>
 __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
                                                  int i, int ptid, I8WsWindow<G>& wCur, const Pre& pre = Pre{},
                                                  unsigned long long* st = nullptr) {
@@ -321,7 +328,13 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 #if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
   unsigned long long t0s = __builtin_amdgcn_s_memtime(), t1s;
 #endif
+#ifdef W4TR
+  if (ptid < kWave) { W4TR(1, i, 0) }
+#endif
   pre();
+#ifdef W4TR
+  if (ptid < kWave) { W4TR(1, i, 1) }
+#endif
 #if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
   if (st) { t1s = __builtin_amdgcn_s_memtime(); st[0] += t1s - t0s; t0s = t1s; }
 #endif
@@ -333,6 +346,9 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 #if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
   if (st) { t1s = __builtin_amdgcn_s_memtime(); st[2] += t1s - t0s; t0s = t1s; }
 #endif
+#ifdef W4TR
+  if (ptid < kWave) { W4TR(1, i, 2) }
+#endif
   int8_t* planes = smem + set * 2 * a.planeStride;
   const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
 #pragma unroll
@@ -342,8 +358,27 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
                                __builtin_amdgcn_alignbyte(wCur.q[j].z, wCur.q[j].y, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.q[j].w, wCur.q[j].z, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.e[j], wCur.q[j].w, a.sub)};
+    if constexpr (Q8) {
+      uint2 iu, qu;
+      int8IqToI8Units(words, iu, qu);
+      const int gg = g < Wl ? g : a.Wu;  // spare unit Wu (even): slot Wu / 2, never read
+      const int off = 16 * cfPhys(gg >> 1, a.padShift) + 8 * (gg & 1);
+      if (!(GSDR_WS_ABL & 4)) {
+        *reinterpret_cast<uint2*>(planes + off) = iu;
+        *reinterpret_cast<uint2*>(planes + a.planeStride + off) = qu;
+      } else {
+        asm volatile("" ::"v"(iu.x), "v"(iu.y), "v"(qu.x), "v"(qu.y));
+      }
+      wsI8LoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
+      continue;
+    }
     uint4 iu, qu;
-    int8IqToF16Units(words, iu, qu);
+    if (GSDR_WS_ABL & 8) {  // timing ablation: no conversion VALU
+      iu = uint4{words[0], words[1], words[2], words[3]};
+      qu = iu;
+    } else {
+      int8IqToF16Units(words, iu, qu);
+    }
     const int off = 16 * cfPhys(g < Wl ? g : a.Wu, a.padShift);  // spare unit Wu: never read
     if (!(GSDR_WS_ABL & 4)) {
       *reinterpret_cast<uint4*>(planes + off) = iu;
@@ -357,6 +392,9 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
   wsSignal(&c->planesFull[set], lane);
 #if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
   if (st) st[3] += __builtin_amdgcn_s_memtime() - t0s;
+#endif
+#ifdef W4TR
+  if (ptid < kWave) { W4TR(1, i, 3) }
 #endif
 }
 
@@ -411,7 +449,8 @@ __device__ __forceinline__ AudioBounds audioBounds(const I8DecArgs& a, int t0, i
 // (called for t = 0, 1, ... in order); ab: audioBounds of the block.
 template <int NSIG = kCfWaves>
 __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* ring, WsCtl* c, int t0, int n, bool lead,
-                                            int t, int ptid, const float (&ht)[kAudioTapsPerLane], AudioBounds& ab) {
+                                            int t, int ptid, const float (&ht)[kAudioTapsPerLane], AudioBounds& ab,
+                                            unsigned long long* st = nullptr) {
   const int lane = ptid & (kWave - 1);
   const int pw = ptid >> 6;
   const int o = lane >> 3, q = lane & 7;
@@ -431,8 +470,14 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
     // except when that call was the lead tile's, which has no outputs and waits for nothing.
     // an aborted launch computes nothing more: its outputs are undefined anyway (the next call fails),
     // and no window is formed from ring slots a finished pipeline would not hold
+#ifdef GSDR_W4_STAMPS
+    const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
+#endif
     bool aborted = wsWaitAb(c, &c->amSlot[t & (kAmRing - 1)], NSIG * (t / kAmRing + 1));
     if (lead && t == 1) aborted |= wsWaitAb(c, &c->amSlot[0], NSIG);
+#ifdef GSDR_W4_STAMPS
+    if (st) st[4] += __builtin_amdgcn_s_memtime() - tw0;  // the ring-slot wait (inside the audio stage's time)
+#endif
 #if GSDR_WS_DIAG
     wsDiag(0, lane == 0 && aborted);
 #endif
@@ -476,14 +521,19 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
         // all 32 reads in flight before the first FMA, then four interleaved partial sums (r05: the
         // compiler had paired the reads into 16 ds_read2_b32, each waited for in full (lgkmcnt(0))
         // before its two FMAs - 16 serialised LDS round trips per batch, ~half of the producers' span)
-        float x[kAudioTapsPerLane];
+        // (taps 2k, 2k + 1 of the lane as one pair: the pair a ds_read2_b32 returns, one v_pk_fma_f32 - r05:
+        // with four scalar partial sums the compiler paired the reads across pairs, 24 v_mov per batch)
+        f2 xv[kAudioTapsPerLane / 2];
 #pragma unroll
-        for (int u = 0; u < kAudioTapsPerLane; ++u) x[u] = w[8 * u];
+        for (int k = 0; k < kAudioTapsPerLane / 2; ++k) xv[k] = f2{w[16 * k], w[16 * k + 8]};
         asm volatile("" ::: "memory");
-        float p4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        f2 a0 = f2{0.0f, 0.0f}, a1 = f2{0.0f, 0.0f};
 #pragma unroll
-        for (int u = 0; u < kAudioTapsPerLane; ++u) p4[u & 3] = fmaf(ht[u], x[u], p4[u & 3]);
-        s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+        for (int k = 0; k < kAudioTapsPerLane / 2; k += 2) {
+          a0 = __builtin_elementwise_fma(f2{ht[2 * k], ht[2 * k + 1]}, xv[k], a0);
+          a1 = __builtin_elementwise_fma(f2{ht[2 * k + 2], ht[2 * k + 3]}, xv[k + 1], a1);
+        }
+        s = (a0.x + a0.y) + (a1.x + a1.y);
       } else {  // windows reaching into the history (the launch's first outputs)
         // buffer loads (range-checked): a pointer select between the ring and the history would
         // compile to FLAT loads
@@ -535,8 +585,11 @@ inline constexpr int kB128Groups[4][16] = {
     {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
 
 // Pick the plane padding and the I/Q plane offset that minimise the A-fragment bank conflicts
-// for this (D, KS), within the LDS budget.
-inline CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes, size_t extra = kCfPartialBytes, int kSteps = 0) {
+// for this (D, KS), within the LDS budget. Wu: 16-byte slots per plane; rowUnits: slots between two
+// A rows (4 D for f16 units of 8 samples, 2 D for int8 slots of 16; 0 = 4 D).
+inline CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes, size_t extra = kCfPartialBytes, int kSteps = 0,
+                              int rowUnits = 0) {
+  if (rowUnits <= 0) rowUnits = 4 * D;
   CfLayout best{4, 0};
   double bestCost = 1e30;
   for (int p = 4; p >= 1; --p) {
@@ -553,7 +606,7 @@ inline CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes, size_t extra =
           int worst = 1;
           for (int li = 0; li < 16; ++li) {
             const int l = grp[li];
-            const int u = 4 * D * (l & 15) + 2 * s + (l >> 5);
+            const int u = rowUnits * (l & 15) + 2 * s + (l >> 5);
             const int unit = u + (u >> p) + (((l >> 4) & 1) ? stride / 16 : 0);
             const int slot = unit & 15;
             bool dup = false;

@@ -4,7 +4,7 @@ AM-epilogue launch (gsdrFirFCAmDemod) at the C3 shape? HIP events around `reps` 
 arms interleaved over rounds, input slots rotating past the 256 MB Infinity Cache (as bench.py).
 Arms: am (the headline launch), cplx (gsdrFirFC only), cplx+am (gsdrFirFC then gsdrQuadAmDemod),
 amk (gsdrQuadAmDemod alone over the cf32 intermediate). Run under rocprofv3 --kernel-trace --stats
-to see the kernels (tools/gpu_r04_a.sh)."""
+to see the kernels (r04: under rocprofv3 --kernel-trace)."""
 import os
 import sys
 import time

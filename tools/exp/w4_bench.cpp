@@ -113,22 +113,61 @@ int main() {
     printf("%-28s median %8.2f us/launch (min %8.2f, max %8.2f)  rel diff vs %s %.3g  %s\n", vars[v].name, s[s.size() / 2],
            s.front(), s.back(), vars[0].name, diff / mx, hipGetErrorString(e));
     if (vars[v].stamps) {  // GSDR_W4_STAMPS build: one more launch, phase cycles per wave
-      const size_t ns = 256 * 8 * 9;
+      const size_t ns = 256 * 8 * 9 + 2 * 128 * 4;
       std::vector<unsigned long long> w(ns, 0);
       vars[v].stamps(w.data(), ns, 1);
       vars[v].fn(&a, ksteps, 0);
       vars[v].stamps(w.data(), ns, 1);
       const char* cn[8] = {"planesFull wait", "partsFull wait", "MFMA loop", "signals", "partsFree wait",
                            "partials write", "epilogue", "last reduce"};
-      const char* pn[4] = {"audio", "window wait", "planesFree wait", "convert+writes+loads"};
+      const char* pn[5] = {"audio", "window wait", "planesFree wait", "convert+writes+loads", "(of audio: ring-slot wait)"};
       for (int role = 0; role < 2; ++role) {
         double tot[9] = {};
         for (int g = 0; g < 256; ++g)
           for (int wv = 4 * role; wv < 4 * role + 4; ++wv)
             for (int k = 0; k < 9; ++k) tot[k] += (double)w[(g * 8 + wv) * 9 + k];
         printf("   %s: span %.0f cycles/wave;", role ? "producers" : "consumers", tot[8] / 1024.0);
-        for (int k = 0; k < (role ? 4 : 8); ++k) printf(" %s %.1f%%", role ? pn[k] : cn[k], 100.0 * tot[k] / tot[8]);
+        for (int k = 0; k < (role ? 5 : 8); ++k) printf(" %s %.1f%%", role ? pn[k] : cn[k], 100.0 * tot[k] / tot[8]);
         printf("\n");
+      }
+      // per-tile trace of block 128: consumer wave 0 e0 loop start, e1 loop end (+ limb combine), e2 tile end;
+      // producer wave 4 f0 tile start, f1 audio done, f2 planesFree seen, f3 planesFull signalled
+      const unsigned long long* tr = w.data() + 256 * 8 * 9;
+      auto C = [&](int i, int e) { return (double)tr[i * 4 + e]; };
+      auto P = [&](int i, int e) { return (double)tr[(128 + i) * 4 + e]; };
+      double s[10] = {};
+      int cnt = 0;
+      for (int i = 10; i < 80; ++i) {
+        if (!C(i, 0) || !P(i, 3) || !C(i + 1, 0)) break;
+        s[0] += C(i, 1) - C(i, 0);      // loop
+        s[1] += C(i, 2) - C(i, 1);      // post
+        s[2] += C(i + 1, 0) - C(i, 2);  // top of next tile (waits)
+        s[3] += C(i, 0) - P(i, 3);      // loop start after planes signalled
+        s[4] += P(i, 1) - P(i, 0);      // producer audio
+        s[5] += P(i, 2) - P(i, 1);      // producer window + planesFree wait
+        s[6] += P(i, 3) - P(i, 2);      // producer convert + writes + signal
+        s[7] += P(i, 2) - C(i - 2, 1);  // planesFree seen after consumer loop i-2 end
+        s[8] += C(i + 1, 0) - C(i, 0);  // period
+        s[9] += C(i + 1, 0) - C(i + 1, 3);  // from the readiness check to the loop start
+        ++cnt;
+      }
+      if (cnt) {
+        const char* nm[9] = {"C loop", "C post", "C top-wait", "C start - P planesFull", "P audio", "P window+planesFree wait",
+                             "P convert", "P planesFree seen - C loop(i-2) end", "period"};
+        printf("   trace (block 128, tiles 10-%d, mean cycles):", 10 + cnt - 1);
+        for (int k = 0; k < 9; ++k) printf(" %s %.0f;", nm[k], s[k] / cnt);
+        printf(" ready->loop %.0f\n", s[9] / cnt);
+        int nr = 0, npf = 0, npp = 0;
+        for (int i = 10; i < 10 + cnt; ++i) {
+          const unsigned long long f = tr[i * 4 + 3] & 7ull;
+          nr += (f & 1) ? 0 : 1; npf += (f & 2) ? 0 : 1; npp += (f & 4) ? 0 : 1;
+        }
+        printf("   not ready at the top: %d of %d tiles (planesFull not reached %d, partsFull %d)\n", nr, cnt, npf, npp);
+        printf("   tiles 20-27 (cycles from C(20) loop start): \n");
+        const double t0 = C(20, 0);
+        for (int i = 20; i < 28; ++i)
+          printf("     %d: C %7.0f %7.0f %7.0f | P %7.0f %7.0f %7.0f %7.0f\n", i, C(i, 0) - t0, C(i, 1) - t0, C(i, 2) - t0,
+                 P(i, 0) - t0, P(i, 1) - t0, P(i, 2) - t0, P(i, 3) - t0);
       }
     }
     if (vars[v].waits) {  // GSDR_WS_WAITS build: one more launch with the counters reset

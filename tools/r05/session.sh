@@ -7,6 +7,7 @@
 #   c5ab       C5 bench, 4-way vs 8-way int8 kernel (2 interleaved rounds)
 #   bench      the default bench line                    prof      rocprofv3 kernel-trace of the default bench
 #   hostfed    rocprofv3 kernel + memory-copy trace of the host-fed C5 leg
+#   hostapi    the same with the HIP runtime API trace (which call blocks the host)
 #   waits      hand-off wait profile of the C5 launch, 4-way and 8-way (waits library)
 #   t:EXPR     the -m gpu tests selected by -k EXPR
 #   ranks8     bench --gpus 8 --share-gpu --backend gloo (the driver's multi-rank path, 8 ranks on cuda:0)
@@ -46,6 +47,8 @@ for s in "$@"; do
             python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
     hostfed) step hostfed 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/hostfed" -o run -- \
                python3 tools/exp/host_fed_probe.py ;;
+    hostapi) step hostapi 300 rocprofv3 --hip-runtime-trace --kernel-trace --memory-copy-trace --output-format csv \
+               -d "$OUT/hostapi" -o run -- python3 tools/exp/host_fed_probe.py ;;
     waits) GSDR_LIB=$PWD/tools/exp/_ablib/waits/libgpusdrpipeline.so step c5_waits_ws4 300 python3 -u tools/exp/c5_waits_probe.py
            GSDR_LIB=$PWD/tools/exp/_ablib/waits/libgpusdrpipeline.so step c5_waits_ws8 300 python3 -u tools/exp/c5_waits_probe.py --ws8 ;;
     t:*) step "test_${s#t:}" 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "${s#t:}" ;;
