@@ -48,7 +48,6 @@ METRIC = "Msamples/sec through FIR→QuadAmDemod chain at 1/2/4/8 MI355X; % HBM 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, spec
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md, FP32 vector (packed FMA)
 F16_PEAK_TFLOPS = 2500.0       # MI355X_MICROARCH.md, BF16/F16 MFMA dense
-I8_PEAK_TOPS = 5000.0          # MI355X_MICROARCH.md: i8 MFMA at 2x the BF16 rate (2x K per instruction)
 
 WORKLOADS = {
     # name: (description, input kind, samples per GPU step, taps, decimation, cutoff, window, fs)
@@ -311,13 +310,13 @@ def kernel_compute(cls, n_out, T, D):
         s = (T + 62) // 32  # K-blocks of 32: K = 32 S >= T + 31
         return ("f16 MFMA (2 tap limbs, fp32 accumulate)", n_out * 2 * 2 * 32 * s * 2, F16_PEAK_TFLOPS)
     if cls == "i8-dec-mfma":
-        # r05 4-way kernel, int8 x int8 form (fir_i8_ws4.hip, GSDR_W4_Q8): the smallest instantiated K
-        # quarter of 32-wide steps that covers 31 D + T (kW4KS), three tap limbs, int32 accumulate
-        ksteps = -(-(31 * D + T) // 32)
+        # r05 4-way kernel (fir_i8_ws4.hip): the smallest instantiated K quarter of 16-wide steps that
+        # covers 31 D + T (kW4KS), two f16 tap limbs, fp32 accumulate
+        ksteps = -(-(31 * D + T) // 16)
         need = -(-ksteps // 4)
-        k_pad = 4 * 32 * min(k for k in (1, 2, 3, 4, 6, 8, 11) if k >= need)
-        return (f"i8 MFMA (int8 samples x 3 signed-byte tap limbs, padded Toeplitz K = {k_pad}, exact int32 "
-                f"accumulate)", n_out * 2 * k_pad * 3 * 2, I8_PEAK_TOPS)
+        k_pad = 4 * 16 * min(k for k in (2, 4, 6, 8, 11, 14, 17, 21, 22) if k >= need)
+        return (f"f16 MFMA (split precision, 2 products, padded Toeplitz K = {k_pad}, fp32 accumulate)",
+                n_out * 2 * k_pad * 2 * 2, F16_PEAK_TFLOPS)
     if cls == "cf-mfma":
         ksteps = -(-(31 * D + T) // 16)  # Toeplitz K in steps of 16; 8 consumer waves, KS K-steps each
         k_pad = 8 * 16 * -(-ksteps // 8)

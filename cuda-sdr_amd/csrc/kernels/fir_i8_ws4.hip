@@ -13,16 +13,10 @@
 // (42 at C5's shape), and 4 partials per output (16 KB per tile) instead of 8. The producers (one
 // wave per SIMD) are firI8WsKernel's: int8 window loads, f16 planes, the fused audio stage.
 //
-// r05 product form (GSDR_W4_Q8 = 1, below): the int8 x int8 MFMA with the taps as three signed-byte limbs
-// of a 22-bit integer - 33 v_mfma_i32_32x32x32_i8 per consumer wave and tile at C5 instead of 42
-// v_mfma_f32_32x32x16_f16, three independent accumulator chains (a single dependent 32x32 chain issues
-// every ~48 cycles, interleaved chains every ~33: tools/exp/mfma_valu_overlap.hip), int8 planes (half
-// the plane bytes and A-fragment reads), and the K sums of a wave exact in int32.
-//
-// Summation: each consumer wave sums its K range (exactly, Q8), and the reduction adds the 4 partials in
-// wave order; the plain and the fused entry points run the same consumer code, so the fused chain's AM
-// samples equal gsdrInt8FirFCAmDemod's bit for bit (the 8-way kernel and the barrier-synchronous one
-// group the K sums differently and round the taps to f16 limbs: same error bound, other rounding).
+// Summation: each consumer wave accumulates its K range in one MFMA chain, and the reduction adds
+// the 4 partials in wave order; the plain and the fused entry points run the same consumer code, so
+// the fused chain's AM samples equal gsdrInt8FirFCAmDemod's bit for bit (the 8-way kernel and the
+// barrier-synchronous one group the K sums differently: same error bound, other rounding).
 #include <algorithm>
 #include <mutex>
 #include <vector>
@@ -45,9 +39,6 @@ __shared__ unsigned long long w4Trace[2 * kW4TraceTiles * 4];
 #define W4TR(role, tile, ev)                                                       \
   if ((threadIdx.x & 63) == 0 && (tile) >= 0 && (tile) < kW4TraceTiles)            \
     w4Trace[((role) * kW4TraceTiles + (tile)) * 4 + (ev)] = __builtin_amdgcn_s_memtime();
-#define W4TRV(role, tile, ev, val)                                                 \
-  if ((threadIdx.x & 63) == 0 && (tile) >= 0 && (tile) < kW4TraceTiles)            \
-    w4Trace[((role) * kW4TraceTiles + (tile)) * 4 + (ev)] = (__builtin_amdgcn_s_memtime() & ~7ull) | (val);
 #endif
 #include "ws_common.h"
 
@@ -63,13 +54,17 @@ constexpr int kW4Sets = GSDR_W4_SETS;  // plane sets: the producers fill tile i 
 constexpr int kW4Threads = (kW4Consumers + kWsProducers) * kWave;  // 512
 constexpr int kW4PartialBytes = kW4Consumers * 16 * kWave * 4;     // 16 KB per partial buffer
 #ifndef GSDR_W4_Q8
-#define GSDR_W4_Q8 1
+#define GSDR_W4_Q8 0
 #endif
-// Q8: the int8 x int8 form - v_mfma_i32_32x32x32_i8 on the int8 samples (the reference's clamp of -128
-// applied), the taps as one 22-bit integer H = round(h 2^sh) split into three signed bytes
-// H = 65536 H0 + 256 H1 + H2, one int32 accumulator per limb (exact: |x H_l| sums over a wave's K
-// quarter stay below 2^24, so each converts to float exactly), combined in fp32 per wave. A K-step is
-// 32 wide (K-steps of 16 below otherwise): 3 MFMAs per 32 taps instead of 2 per 16, int8 planes.
+// Q8 (build option, not the product: DESIGN.md 5.1): the int8 x int8 form - v_mfma_i32_32x32x32_i8 on the
+// int8 samples (the reference's clamp of -128 applied), the taps as one 24-bit integer H = round(h 2^sh)
+// (|H| < 2^23) split into three signed bytes H = 65536 H0 + 256 H1 + H2, one int32 accumulator per limb
+// (exact: |x H_l| sums over a wave's K quarter stay below 2^24, so each converts to float exactly),
+// combined in fp32 per wave. A K-step is 32 wide (16 otherwise): 3 MFMAs per 32 taps instead of 2 per 16,
+// three independent accumulator chains, int8 planes - 11-13 % faster at C5, but the tap rounding is
+// relative to the largest tap, and for long filters with wide passbands the output's relative L2 error
+// reaches the 1e-6 bar (1.03e-6 at T = 1023, D = 3; 4.8e-7 at C5's filter), where the f16 limbs keep
+// each tap to 2^-22 of itself.
 constexpr bool kW4Q8 = GSDR_W4_Q8 != 0;
 constexpr int kW4KStep = kW4Q8 ? 32 : 16;                            // taps per consumer K-step
 constexpr int kW4MaxKS = kW4Q8 ? 11 : 22;                            // K <= 4 x 11 x 32 = 4 x 22 x 16 = 1408
@@ -157,34 +152,37 @@ __device__ __forceinline__ void w4AmFreeWait(WsCtl* c, int j) {  // ring slot of
   if (j - kAmRing + 2 > 0) wsWait(c, &c->amFree, kWsProducers * (j - kAmRing + 2));
 }
 
-#ifndef GSDR_W4_CPRIO  // Q8: 0 (r05: 128.9-131.4 vs 130.4-136.4 us at priority 1); f16 form: 1
+#ifndef GSDR_W4_LATESIG
+#define GSDR_W4_LATESIG 1  // A/B switch: outputs formed between the partial writes and their signal
+#endif
+#ifndef GSDR_W4_CPRIO  // f16 form: 1 (r05: 142.9-146.7 vs 144.3-149.6 us); Q8: 0 (128.9-131.4 vs 130.4-136.4)
 #define GSDR_W4_CPRIO (GSDR_W4_Q8 ? 0 : 1)
 #endif
-// Partial-sum buffers: tile i's partials go to buffer i % 3 and are reduced in tile i + 2's K loop, so a
-// wave never waits for the other consumer waves' partials of the tile it has just finished (r05 trace:
-// with the reduction one tile behind, the four waves met every tile, ~600 cycles of waiting per tile).
-constexpr int kW4PartBufs = 3;
-// the producers compute the audio of tile p - kW4AudioLag at their tile p: the ring holds tile j once the
-// consumers are past tile j + 3, and a producer at tile p has seen the consumers past tile p - 3
-constexpr int kW4AudioLag = 6;
-
-// The three hand-off counters a consumer tile starts on (planesFull, partsFull, amFree) checked in ONE LDS
-// round trip (the loads issued together, one wait): true when all have reached their targets (the
-// caller then skips the individual waits, three serial round trips; they are almost always satisfied).
-__device__ __forceinline__ bool w4Ready(const int* p0, int g0, const int* p1, int g1, const int* p2, int g2) {
+#ifndef GSDR_W4_NOFENCE  // A/B: hand-offs ordered by the LDS queue alone (no lgkmcnt(0) before a signal)
+#define GSDR_W4_NOFENCE 0
+#endif
+#ifndef GSDR_W4_READY
+#define GSDR_W4_READY 1  // A/B switch of the one-round-trip readiness check below
+#endif
+// Up to four hand-off counters checked in ONE LDS round trip (the four loads issued together, one wait):
+// true when every counter has reached its target (the caller then skips the individual waits). A
+// consumer wave starts each tile waiting on planesFull, partsFull, amFree and partsFree - one after the
+// other that was four serial LDS round trips per tile, and they are almost always already satisfied.
+__device__ __forceinline__ bool w4Ready(WsCtl* c, const int* p0, int g0, const int* p1, int g1, const int* p2, int g2,
+                                        const int* p3, int g3) {
   const int v0 = __hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   const int v1 = __hip_atomic_load(p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   const int v2 = __hip_atomic_load(p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return waveUniform(v0) >= g0 && waveUniform(v1) >= g1 && waveUniform(v2) >= g2;
+  const int v3 = __hip_atomic_load(p3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return waveUniform(v0) >= g0 && waveUniform(v1) >= g1 && waveUniform(v2) >= g2 && waveUniform(v3) >= g3;
 }
 
-// The consumer waves: B fragments of this wave's K quarter in VGPRs for the whole launch, then per tile i
-// its K-quarter MFMAs with tile i - 2's reduction folded in - its four partial reads issued and summed in
-// the gaps between the MFMAs - and, for the fused chain, the AM ring writes of tile i - 3; then tile i's
-// partials (signalled at the top of tile i + 1, whose readiness check has drained them) and tile i - 2's
-// outputs formed in registers. (r05 stamps: as separate phases the reduction, the partial writes and the
-// epilogue took ~40 % of a consumer wave's span beside 43 % for its MFMAs: with one consumer wave per
-// SIMD nothing hid their LDS round trips.)
+// The consumer waves: B fragments of this wave's K quarter in VGPRs for the whole launch, then per tile
+// 2 KS MFMAs with the previous tile's reduction folded in - its four partial reads issued and summed in
+// the gaps between this tile's MFMAs - and, for the fused chain, the AM ring writes of the tile before
+// that (r05 stamps: as separate phases the reduction, the partial writes and the epilogue took ~40 % of a
+// consumer wave's span beside 43 % for its MFMAs: with one consumer wave per SIMD nothing hid their LDS
+// round trips); then the partials of this tile, and the previous tile's outputs formed in registers.
 template <int KS, int EPI, bool AUD>
 __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* smem, float* part, WsCtl* c, int sh,
                                             int t0, int n, int tid, float* ring, bool lead) {
@@ -203,11 +201,11 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
     uint32_t w0[4] = {0, 0, 0, 0}, w1[4] = {0, 0, 0, 0}, w2[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int H = (int)rintf(ldexpf(part[off0 + kap + e - col * D], sh));  // |H| < 2^22
+      const int H = (int)rintf(ldexpf(part[off0 + kap + e - col * D], sh));  // |H| <= 8 355 711
       const int h2 = (int)(int8_t)(H & 0xff);
       const int r1 = (H - h2) >> 8;
       const int h1 = (int)(int8_t)(r1 & 0xff);
-      const int h0 = (r1 - h1) >> 8;  // |h0| <= 64
+      const int h0 = (r1 - h1) >> 8;  // in [-128, 127]
       w0[e >> 2] |= (uint32_t)(h0 & 0xff) << (8 * (e & 3));
       w1[e >> 2] |= (uint32_t)(h1 & 0xff) << (8 * (e & 3));
       w2[e >> 2] |= (uint32_t)(h2 & 0xff) << (8 * (e & 3));
@@ -240,7 +238,7 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
   const int comp = (lane >> 4) & 1;
   const int uRow = (kW4Q8 ? 2 : 4) * D * arow + half;  // A row arow: 32 D samples = 2 D int8 / 4 D f16 slots
   const float outScale = ldexpf(1.0f / 127.0f, -sh);
-  float am[2] = {0.0f, 0.0f};  // AUD: AM samples of tile i - 3 (this lane's), written to the ring in tile i's loop
+  float am[2] = {0.0f, 0.0f};  // AUD: AM samples of tile i - 2 (this lane's), written to the ring in tile i's loop
 #ifdef GSDR_W4_STAMPS
   unsigned long long cst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tlast = __builtin_amdgcn_s_memtime();
@@ -248,39 +246,24 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
 #endif
   for (int i = 0; i < n; ++i) {
     const int set = i % kW4Sets;
-    const int jr = i - 2;                           // the tile reduced in this tile's K loop
-    const bool red = jr >= 0;
-    const int rb = (i + 1) % kW4PartBufs;           // = jr mod 3
-    const int jw = i - 3;                           // the tile whose AM samples go to the ring in it
-    const bool ringW = AUD && jw >= 0;
-    const int b = i % kW4PartBufs;                  // this tile's partial buffer: tile i - 3's, reduced in tile i - 1
+    const bool red = i >= 1;           // tile i - 1's partials (all four waves': each wrote them before its tile i)
+    const int rb = (i - 1) & 1;
+    const bool ringW = AUD && i >= 2;  // tile i - 2's AM samples go to the ring in this loop
+    const int b = i & 1;               // this tile's partial buffer: free once tile i - 2 is reduced
     const int gFull = kWsProducers * (i / kW4Sets + 1);
-    const int gParts = red ? kW4Consumers * (jr / kW4PartBufs + 1) : 0;
-    const int gAm = ringW && jw - kAmRing + 2 > 0 ? kWsProducers * (jw - kAmRing + 2) : 0;
-    // before tile i - 3 exists the buffer is free once every wave has read the taps staged there
-    int* const pFree = i >= kW4PartBufs ? &c->partsFree[b] : &c->tapsRead;
-    const int gFree = i >= kW4PartBufs ? kW4Consumers * (i / kW4PartBufs) : kW4Consumers;
-    // the partial buffer's counter is read here and checked after the K loop, where it is needed (the
-    // other waves free it at the end of their tile i - 1: folded into the check above, it failed whenever
-    // one of them was a little behind, and the slow path cost three more round trips)
-    const int vFree = __hip_atomic_load(pFree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const bool ready = w4Ready(&c->planesFull[set], gFull, &c->partsFull[rb], gParts, &c->amFree, gAm);
-#ifdef GSDR_W4_STAMPS
-    if (wave == 0) {
-      const int pf = waveUniform(__hip_atomic_load(&c->planesFull[set], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= gFull;
-      const int pp = waveUniform(__hip_atomic_load(&c->partsFull[rb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= gParts;
-      W4TRV(0, i, 3, (ready ? 1 : 0) | (pf ? 2 : 0) | (pp ? 4 : 0))
-    }
-#endif
-    // tile i - 1's partials, written before the check above (its wait drained them: the fence costs nothing
-    // more), for the waves that reduce them in tile i + 1 - signalled before any wait of this wave
-    if (i >= 1) wsSignal(&c->partsFull[(i - 1) % kW4PartBufs], lane);
+    const int gParts = red ? kW4Consumers * (((i - 1) >> 1) + 1) : 0;
+    const int gAm = ringW && i - 2 - kAmRing + 2 > 0 ? kWsProducers * (i - 2 - kAmRing + 2) : 0;
+    // the partial buffer: free once tile i - 2 is reduced (before that: once the tap staging area is read)
+    int* const pFree = i >= 2 ? &c->partsFree[b] : &c->tapsRead;
+    const int gFree = i >= 2 ? kW4Consumers * (i >> 1) : kW4Consumers;
+    const bool ready = GSDR_W4_READY && w4Ready(c, &c->planesFull[set], gFull, &c->partsFull[rb], gParts, &c->amFree, gAm, pFree, gFree);
     if (ready) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      if (GSDR_W4_NOFENCE) asm volatile("" ::: "memory");
+      else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     } else {
       wsWait(c, &c->planesFull[set], gFull);
       if (red) wsWait(c, &c->partsFull[rb], gParts);
-      if (ringW) w4AmFreeWait(c, jw);
+      if (ringW) w4AmFreeWait(c, i - 2);
     }
     W4ST(0)
     W4ST(1)
@@ -299,43 +282,35 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
     f4 pv[kW4Consumers];
     f4 y = f4{0.0f, 0.0f, 0.0f, 0.0f};
     auto readA = [&](int s) {
-      if (GSDR_WS_ABL & 32) {  // timing ablation: no A reads
-        xa[s] = AFrag{};
-        asm volatile("" : "+v"(xa[s]));
-      } else {
-        xa[s] = *reinterpret_cast<const AFrag*>(pI + 16 * cfPhys(uRow + 2 * (wave * KS + s), a.padShift));
-      }
+      xa[s] = *reinterpret_cast<const AFrag*>(pI + 16 * cfPhys(uRow + 2 * (wave * KS + s), a.padShift));
     };
-    // (the partial reads are unconditional - no branch in the K loop; for i < 2 they read a buffer
+    // (the partial reads are unconditional - no branch in the K loop; at i = 0 they read buffer 1,
     // whatever it holds, and the sums are not used)
-    auto readP = [&](int v) {
-      if (GSDR_WS_ABL & 16) {  // timing ablation: no partial exchange
-        pv[v] = f4{1.0f, 1.0f, 1.0f, 1.0f};
-        asm volatile("" : "+v"(pv[v]));
-      } else {
-        pv[v] = *w4Part(part, rb, v, wave, lane);
-      }
-    };
+    auto readP = [&](int v) { pv[v] = *w4Part(part, rb, v, wave, lane); };
 #pragma unroll
     for (int s = 0; s < PF; ++s) readA(s);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       if (s + PF < KS) readA(s + PF);
       if (s < kW4Consumers) readP(s);
-      if (s == 0 && ringW) w4RingWrite(ring, jw, tid, am);
+      if (s == 0 && ringW) w4RingWrite(ring, i - 2, tid, am);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #if GSDR_W4_Q8
-      if (GSDR_WS_ABL & 64) {  // timing ablation: no MFMAs
-        asm volatile("" ::"v"(xa[s]), "v"(b0[s]), "v"(b1[s]), "v"(b2[s]));
-      } else {
-        acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[s], b0[s], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[s], b1[s], acc1, 0, 0, 0);
-        acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[s], b2[s], acc2, 0, 0, 0);
-      }
+      acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[s], b0[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[s], b1[s], acc1, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[s], b2[s], acc2, 0, 0, 0);
 #else
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bh[s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bl[s], acc, 0, 0, 0);
+      if (!(GSDR_WS_ABL & 1)) {
+#pragma unroll
+        for (int rep = 0; rep < GSDR_WS_MFREP; ++rep) {  // timing experiments: MFMA work x MFREP
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bh[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s], bl[s], acc, 0, 0, 0);
+        }
+      } else {
+        asm volatile("" ::"v"(xa[s]));
+        acc[s & 15] += 1.0f;
+      }
 #endif
       __builtin_amdgcn_sched_barrier(0);
       if (s >= 2 && s - 2 < kW4Consumers) y += pv[s - 2];  // writer order: v = s - 2
@@ -356,50 +331,62 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
 #ifdef GSDR_W4_STAMPS
     if (wave == 0) { W4TR(0, i, 1) }
 #endif
-    // one release for the three hand-offs (their LDS reads and writes were all waited for in the loop)
+    // one release for the three hand-offs (their LDS reads and writes were all waited for in the loop);
+    // fenced one by one, each signal waited out the previous one's LDS atomic
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    wsSignalNF(&c->planesFree[set], lane);                           // this wave's A reads are complete
-    if (red) wsSignalNF(&c->partsFree[rb], lane);                    // and its reads of tile i - 2's partials
-    if (ringW) wsSignalNF(&c->amSlot[jw & (kAmRing - 1)], lane);     // tile i - 3 is in the ring
+    wsSignalNF(&c->planesFree[set], lane);         // this wave's A reads are complete
+    if (red) wsSignalNF(&c->partsFree[rb], lane);  // and its reads of tile i - 1's partials
+    if (ringW) wsSignalNF(&c->amSlot[(i - 2) & (kAmRing - 1)], lane);  // tile i - 2 is in the ring
     W4ST(3)
-    if (waveUniform(vFree) < gFree) wsWait(c, pFree, gFree);  // tile i - 3 reduced by every wave
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    if (!ready) wsWait(c, pFree, gFree);  // tile i - 2 reduced by every wave (almost always seen above)
     W4ST(4)
     f4* pb = reinterpret_cast<f4*>(part + b * (kW4PartialBytes / 4));
 #pragma unroll
     for (int r = 0; r < kW4Consumers; ++r)
-      if (!(GSDR_WS_ABL & 16)) pb[(wave * 4 + r) * kWave + lane] = f4{acc[r], acc[r + 4], acc[r + 8], acc[r + 12]};
+      if (!(GSDR_WS_ABL & 2)) pb[(wave * 4 + r) * kWave + lane] = f4{acc[r], acc[r + 4], acc[r + 8], acc[r + 12]};
       else asm volatile("" ::"v"(acc[r]), "v"(acc[r + 4]), "v"(acc[r + 8]), "v"(acc[r + 12]));
-    W4ST(5)
-    if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + jr, jr, tid, y, lead, am);
+#if GSDR_W4_LATESIG  // the previous tile's outputs while the partial writes land
+    if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am);
     W4ST(6)
+    if (GSDR_W4_NOFENCE) {
+      asm volatile("" ::: "memory");
+      wsSignalNF(&c->partsFull[b], lane);
+    } else {
+      wsSignal(&c->partsFull[b], lane);
+    }
+    W4ST(5)
+#else
+    wsSignal(&c->partsFull[b], lane);
+    W4ST(5)
+    if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am);
+    W4ST(6)
+#endif
 #ifdef GSDR_W4_STAMPS
     if (wave == 0) { W4TR(0, i, 2) }
 #endif
   }
-  if (n >= 1) wsSignal(&c->partsFull[(n - 1) % kW4PartBufs], lane);  // the last tile's partials
-  if constexpr (AUD) {  // tile n - 3 (pending) into the ring
-    if (n >= 3) {
-      w4AmFreeWait(c, n - 3);
-      w4RingWrite(ring, n - 3, tid, am);
-      wsSignal(&c->amSlot[(n - 3) & (kAmRing - 1)], lane);
+  if constexpr (AUD) {  // tile n - 2 (pending) into the ring
+    if (n >= 2) {
+      w4AmFreeWait(c, n - 2);
+      w4RingWrite(ring, n - 2, tid, am);
+      wsSignal(&c->amSlot[(n - 2) & (kAmRing - 1)], lane);
     }
   }
-  for (int j = n >= 2 ? n - 2 : 0; j < n; ++j) {  // the last two tiles' reductions on their own
-    const int rbj = j % kW4PartBufs;
-    wsWait(c, &c->partsFull[rbj], kW4Consumers * (j / kW4PartBufs + 1));
+  if (n >= 1) {  // the last tile's reduction on its own
+    const int j = n - 1, rb = j & 1;
+    wsWait(c, &c->partsFull[rb], kW4Consumers * ((j >> 1) + 1));
     f4 y = f4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int v = 0; v < kW4Consumers; ++v) y += *w4Part(part, rbj, v, wave, lane);
-    wsSignal(&c->partsFree[rbj], lane);
+    for (int v = 0; v < kW4Consumers; ++v) y += *w4Part(part, rb, v, wave, lane);
+    wsSignal(&c->partsFree[rb], lane);
     w4Outputs<EPI, AUD>(a, outScale, t0 + j, j, tid, y, lead, am);
     if constexpr (AUD) {
       w4AmFreeWait(c, j);
       w4RingWrite(ring, j, tid, am);
       wsSignal(&c->amSlot[j & (kAmRing - 1)], lane);
     }
+    W4ST(7)
   }
-  W4ST(7)
 #ifdef GSDR_W4_STAMPS
   if ((int)blockIdx.x == kW4TraceBlock && wave == 0 && lane == 0)
     for (int k = 0; k < kW4TraceTiles * 4; ++k) gW4Stamps[kW4StampWords + k] = w4Trace[k];
@@ -414,7 +401,7 @@ template <int KS, int G, int EPI, bool AUD>
 __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, int Wl) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   float* part = reinterpret_cast<float*>(smem + 2 * kW4Sets * a8.planeStride);
-  float* ring = AUD ? reinterpret_cast<float*>(smem + 2 * kW4Sets * a8.planeStride + kW4PartBufs * kW4PartialBytes) : nullptr;
+  float* ring = AUD ? reinterpret_cast<float*>(smem + 2 * kW4Sets * a8.planeStride + 2 * kW4PartialBytes) : nullptr;
   __shared__ WsCtl ctl;
   __shared__ float waveMax[kW4Consumers + kWsProducers];
   WsCtl* c = &ctl;
@@ -465,8 +452,10 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
   float hMax = waveMax[0];
 #pragma unroll
   for (int v = 1; v < kW4Consumers + kWsProducers; ++v) hMax = fmaxf(hMax, waveMax[v]);
-  // max |h 2^sh| in [2^14, 2^15) (f16 limbs) / [2^21, 2^22) (Q8: three signed bytes, top limb <= 64)
-  const int sh = hMax > 0.0f ? (kW4Q8 ? 21 : 14) - ilogbf(hMax) : 0;
+  // max |h 2^sh| in [2^14, 2^15) (f16 limbs) / below 127 (65536 + 256 + 1) = 8 355 711 (Q8: three signed
+  // bytes; [2^22, 2^23) unless that would overflow the top limb, then half of it)
+  int sh = hMax > 0.0f ? (kW4Q8 ? 22 : 14) - ilogbf(hMax) : 0;
+  if (kW4Q8 && hMax > 0.0f && ldexpf(hMax, sh) > 8355711.0f) --sh;
 #if GSDR_WS_WAITS
   const unsigned long long span0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -507,17 +496,17 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
 #endif
     for (int i = 0;; i += 2) {
       wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
-        if (AUD && i >= kW4AudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i - kW4AudioLag, ptid, ht, ab, stp);
+        if (AUD && i >= kAudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht, ab, stp);
       }, stp);
       if (i + 1 >= n) break;
       wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
-        if (AUD && i + 1 >= kW4AudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i + 1 - kW4AudioLag, ptid, ht, ab, stp);
+        if (AUD && i + 1 >= kAudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht, ab, stp);
       }, stp);
       if (i + 2 >= n) break;
     }
     (void)stp;
     if constexpr (AUD)
-      for (int t = n > kW4AudioLag ? n - kW4AudioLag : 0; t < n; ++t)
+      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t)
         wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, t, ptid, ht, ab);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the wave
 #ifdef GSDR_W4_STAMPS
@@ -653,7 +642,7 @@ hipError_t launchFirI8Ws4(I8DecArgs a, int ksteps, int epi, bool audio, hipStrea
   const int Wl = std::min(a.Wu, (511 * a.D + a.T + 7) / 8);
   if (Wl > 4 * kWsPThreads) return hipErrorNotSupported;
   const size_t ringBytes = audio ? sizeof(float) * (kAmRing * kCfTileOut + kAmRingMirror) : 0;
-  const size_t extra = kW4PartBufs * (size_t)kW4PartialBytes + ringBytes;
+  const size_t extra = 2 * (size_t)kW4PartialBytes + ringBytes;
   // the layout search costs ~1 ms of host time: cached per (D, KS, audio)
   static std::mutex mu;
   static std::vector<std::pair<uint64_t, CfLayout>> cache;

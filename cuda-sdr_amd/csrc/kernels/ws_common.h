@@ -587,8 +587,10 @@ inline constexpr int kB128Groups[4][16] = {
 // Pick the plane padding and the I/Q plane offset that minimise the A-fragment bank conflicts
 // for this (D, KS), within the LDS budget. Wu: 16-byte slots per plane; rowUnits: slots between two
 // A rows (4 D for f16 units of 8 samples, 2 D for int8 slots of 16; 0 = 4 D).
+// blocks16: the 4-way kernel's 16 x 16 x 32 reads (lane l: row l % 16, slot 4 s + l / 16, one plane per
+// read) instead of the 32 x 32 ones (row l % 16, slot 2 s + l / 32, lanes 16-31 of l % 32 in the Q plane).
 inline CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes, size_t extra = kCfPartialBytes, int kSteps = 0,
-                              int rowUnits = 0) {
+                              int rowUnits = 0, bool blocks16 = false) {
   if (rowUnits <= 0) rowUnits = 4 * D;
   CfLayout best{4, 0};
   double bestCost = 1e30;
@@ -606,8 +608,8 @@ inline CfLayout cfPlaneLayout(int D, int KS, int Wu, int nPlanes, size_t extra =
           int worst = 1;
           for (int li = 0; li < 16; ++li) {
             const int l = grp[li];
-            const int u = rowUnits * (l & 15) + 2 * s + (l >> 5);
-            const int unit = u + (u >> p) + (((l >> 4) & 1) ? stride / 16 : 0);
+            const int u = blocks16 ? rowUnits * (l & 15) + 4 * s + (l >> 4) : rowUnits * (l & 15) + 2 * s + (l >> 5);
+            const int unit = u + (u >> p) + (!blocks16 && ((l >> 4) & 1) ? stride / 16 : 0);
             const int slot = unit & 15;
             bool dup = false;
             for (int c = 0; c < cnt[slot]; ++c) dup |= slots[slot][c] == unit;

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""r05: float64 model of the int8 x int8 (Q8) form's tap rounding in fir_i8_ws4.hip (one 24-bit integer
+per tap, |H| < 2^23, scaled to the LARGEST tap) over a grid of tap counts, decimations and windowed-sinc
+low-pass shapes: the max per-element error over the 1e-6 * sum|h||x| bound and the relative L2 error,
+both against the float64 filter of the same float32 taps and int8 IQ input (x = max(q, -127) / 127).
+Worst cases first. Self-contained (numpy / scipy), no GPU."""
+import numpy as np
+from scipy.signal import firwin
+
+rng = np.random.default_rng(7)
+
+
+def fir(h, x, D, n_out):
+    """y[k] = sum_j h[j] x[k D + j] in float64, and sum_j |h[j]| |x[k D + j]|."""
+    idx = np.arange(n_out)[:, None] * D + np.arange(len(h))[None, :]
+    xs = x[idx]
+    return xs @ h, np.abs(xs) @ np.abs(h)
+
+
+def q8_taps(h):
+    hmax = float(np.max(np.abs(h)))
+    sh = 22 - (int(np.frexp(np.float32(hmax))[1]) - 1)
+    if np.ldexp(hmax, sh) > 8355711.0:
+        sh -= 1
+    return np.ldexp(np.rint(np.ldexp(h.astype(np.float64), sh)), -sh)
+
+
+def case(T, D, cutoff, window, n_out=8000):
+    h = firwin(T, min(cutoff, 0.99), window=window).astype(np.float32).astype(np.float64)
+    n_in = (n_out - 1) * D + T
+    q = rng.integers(-128, 128, size=2 * n_in)
+    x = np.maximum(q, -127) / 127.0
+    xc = x[0::2] + 1j * x[1::2]
+    y64, bound = fir(h, xc, D, n_out)
+    yq, _ = fir(q8_taps(h), xc, D, n_out)
+    err = np.abs(yq - y64)
+    return float(np.max(err / (1e-6 * bound))), float(np.linalg.norm(yq - y64) / np.linalg.norm(y64))
+
+
+if __name__ == "__main__":
+    res = []
+    for T in (16, 31, 64, 100, 127, 129, 200, 255, 300, 511, 700, 1023):
+        for D in (2, 3, 4, 5, 8, 10, 16):
+            for cut, win in ((0.8 / D, "hamming"), (0.4 / D, "hamming"), (0.08, "hamming"), (0.08, "blackman"),
+                             (0.2, "hamming"), (0.6 / D, "hamming"), (0.8 / D, "blackman")):
+                w, l2 = case(T, D, cut, win)
+                res.append((max(w, l2 * 1e6), T, D, round(cut, 4), win, round(w, 3), l2))
+    res.sort(reverse=True)
+    print("worst of", len(res), "cases: (max(per-element / bound, L2 / 1e-6), T, D, cutoff (x Nyquist), window, "
+          "per-element / bound, relative L2)")
+    for r in res[:12]:
+        print(r)
