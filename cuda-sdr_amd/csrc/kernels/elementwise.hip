@@ -9,6 +9,8 @@
 // byte offsets).
 #include "kcommon.h"
 
+#include <algorithm>
+
 #include <gsdr/conversion.h>
 #include <gsdr/gsdr.h>
 #include <gsdr/gsdr_amd.h>
@@ -192,6 +194,23 @@ __global__ __launch_bounds__(kBlock) void hbmProbeKernel(const f4* __restrict__ 
   if (MODE == 0 && acc == -1.2345e-38f) out[0] = f4{acc, acc, acc, acc};
 }
 
+// ---- copies between mapped pinned host memory and the device as kernels (the host-fed chain) ---------
+// 16-byte loads from a 16-byte aligned source, stores at any 4-byte aligned destination (global stores
+// of 16 bytes need dword alignment only); the dword kernel for the rest.
+__global__ __launch_bounds__(kBlock) void copyVec16(const uint4* __restrict__ src, uint8_t* __restrict__ dst, size_t n16) {
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += (size_t)gridDim.x * kBlock) {
+    const uint4 v = src[i];
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst + 16 * i);
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  }
+}
+__global__ __launch_bounds__(kBlock) void copyDword(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, size_t n4) {
+  for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += (size_t)gridDim.x * kBlock) dst[i] = src[i];
+}
+
 // ---- LDS poison (tests): fill every CU's LDS with a pattern so a kernel that reads LDS it never
 // wrote shows it (a NaN pattern turns 0 * stale into NaN) ------------------------------------------
 constexpr int kPoisonLdsBytes = 160 * 1024 - 256;
@@ -202,6 +221,24 @@ __global__ __launch_bounds__(1024) void ldsPoisonKernel(uint32_t pattern) {
 }
 
 extern "C" {
+
+hipError_t gsdrAmdCopyKernel(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  if (bytes == 0) return hipSuccess;
+  const auto d = reinterpret_cast<uintptr_t>(dst), s = reinterpret_cast<uintptr_t>(src);
+  if ((d & 3) != 0 || (s & 3) != 0 || (bytes & 3) != 0) return hipErrorInvalidValue;
+  if ((s & 15) == 0 && (bytes & 15) == 0) {
+    const size_t n16 = bytes / 16;
+    const unsigned grid = (unsigned)std::min<size_t>((n16 + kBlock - 1) / kBlock, 2048);
+    hipLaunchKernelGGL(copyVec16, dim3(grid), dim3(kBlock), 0, stream, static_cast<const uint4*>(src),
+                       static_cast<uint8_t*>(dst), n16);
+  } else {
+    const size_t n4 = bytes / 4;
+    const unsigned grid = (unsigned)std::min<size_t>((n4 + kBlock - 1) / kBlock, 2048);
+    hipLaunchKernelGGL(copyDword, dim3(grid), dim3(kBlock), 0, stream, static_cast<const uint32_t*>(src),
+                       static_cast<uint32_t*>(dst), n4);
+  }
+  return hipGetLastError();
+}
 
 hipError_t gsdrAmdPoisonLds(uint32_t pattern, int32_t device, hipStream_t stream) {
   DevicePush push(device);

@@ -97,6 +97,8 @@ struct gsdrAmChainImpl {
   size_t slots = 0;
   int8_t* hostIn = nullptr;
   float* hostOut = nullptr;
+  int8_t* hostInDev = nullptr;  // the same slots as device pointers (hipHostGetDevicePointer)
+  float* hostOutDev = nullptr;
   std::vector<hipEvent_t> slotDone;
 
   size_t nextOutputs() const { return steps == 0 ? na1 : naSteady; }
@@ -270,6 +272,8 @@ hipError_t build(gsdrAmChainImpl* c, const gsdrAmChainConfig& cfg) {
     AMC_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hostIn), 2 * c->L * c->slots, hipHostMallocDefault));
     AMC_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hostOut), sizeof(float) * c->naSteady * c->slots,
                           hipHostMallocDefault));
+    AMC_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hostInDev), c->hostIn, 0));
+    AMC_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->hostOutDev), c->hostOut, 0));
     c->slotDone.assign(c->slots, nullptr);
     for (auto& ev : c->slotDone) AMC_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   }
@@ -421,14 +425,19 @@ hipError_t gsdrAmChainStepHost(gsdrAmChain c, size_t slot, size_t* outputCount) 
   const size_t n = c->nextOutputs();
   // the H2D copy may start once the step that last read staging[p] is done with it
   AMC_TRY(hipStreamWaitEvent(c->copyStream, c->readDone[p], 0));
-  AMC_TRY(hipMemcpyAsync(c->staging[p] + 2 * c->r, c->hostIn + 2 * c->L * slot, 2 * c->L, hipMemcpyHostToDevice,
-                         c->copyStream));
+  // the copies as kernels on the mapped pinned slots: hipMemcpyAsync here blocked the host thread for
+  // 7-10 ms in 10 of ~600 calls (r05 HIP API trace: the DMA itself 0.18 ms, issued at the end of the call)
+  // (an odd r leaves the staging destination 2 bytes off dword alignment: the runtime copy then)
+  if (((2 * c->r) & 3) == 0)
+    AMC_TRY(gsdrAmdCopyKernel(c->staging[p] + 2 * c->r, c->hostInDev + 2 * c->L * slot, 2 * c->L, c->copyStream));
+  else
+    AMC_TRY(hipMemcpyAsync(c->staging[p] + 2 * c->r, c->hostIn + 2 * c->L * slot, 2 * c->L, hipMemcpyHostToDevice,
+                           c->copyStream));
   AMC_TRY(hipEventRecord(c->copyDone[p], c->copyStream));
   AMC_TRY(hipStreamWaitEvent(c->stream, c->copyDone[p], 0));
   AMC_TRY(hipGraphLaunch(c->graphFor(p), c->stream));
   AMC_TRY(hipEventRecord(c->readDone[p], c->stream));
-  AMC_TRY(hipMemcpyAsync(c->hostOut + c->naSteady * slot, c->audio, sizeof(float) * n, hipMemcpyDeviceToHost,
-                         c->stream));
+  AMC_TRY(gsdrAmdCopyKernel(c->hostOutDev + c->naSteady * slot, c->audio, sizeof(float) * n, c->stream));
   AMC_TRY(hipEventRecord(c->slotDone[slot], c->stream));
   ++c->steps;
   if (outputCount != nullptr) *outputCount = n;

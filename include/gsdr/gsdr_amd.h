@@ -195,6 +195,12 @@ GSDR_API hipError_t gsdrAmdHbmProbe(const void* input, void* output, size_t byte
 /* Tests: fill the LDS of every CU of `device` with the 32-bit `pattern` (one workgroup of the whole
  * LDS per slot, 4 per CU) on `stream`, so that a later kernel reading LDS it never wrote sees it. */
 GSDR_API hipError_t gsdrAmdPoisonLds(uint32_t pattern, int32_t device, hipStream_t stream);
+/* A copy as a kernel on `stream`: `src` / `dst` device memory or mapped pinned host memory (device
+ * pointers from hipHostGetDevicePointer), 4-byte aligned, `bytes` a multiple of 4 (16-byte loads when
+ * `src` and `bytes` are 16-byte aligned). The host-fed chain moves its chunks with it: hipMemcpyAsync
+ * between pinned host slots and the device blocked the host thread 7-10 ms in 10 of ~600 calls (r05
+ * HIP API trace), a kernel launch never does. hipErrorInvalidValue on misalignment. */
+GSDR_API hipError_t gsdrAmdCopyKernel(void* dst, const void* src, size_t bytes, hipStream_t stream);
 
 GSDR_API hipError_t gsdrSynthIqInt8(uint64_t seed, double sampleRate, double amToneHz, double carrierHz,
                                     uint64_t firstSample, int8_t* outputIq, size_t numSamples, int32_t device,
