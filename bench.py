@@ -909,13 +909,6 @@ def main():
         del chain
         torch.cuda.empty_cache()
         for wl, k, w in (("c4s", 6, 2), ("c5", 40, 3), ("c2", 400, 5)):
-            if wl == "c5" and world > 1 and os.environ.get("GSDR_BENCH_C5_MULTI") != "1":
-                # r05 late: the sharded C5 step at N > 1 (bulk + head launches around the halo exchange)
-                # faulted (hipErrorIllegalAddress) in 2- and 8-rank runs on one GPU; until that is found
-                # the multi-rank runs skip it rather than lose the whole line
-                extras[wl] = {"skipped": "N > 1 sharded C5 step under investigation (DESIGN.md 9); "
-                                         "GSDR_BENCH_C5_MULTI=1 runs it"}
-                continue
             xc = (AmChainSharded(ops, rank, world, device, stage) if wl == "c5" else
                   ShardedChain(ops, wl, rank, world, device, stage))
             e2, k2, _ = timed_steps(xc, k, w, world, args.backend, device, local, ops)

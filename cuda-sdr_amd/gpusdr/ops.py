@@ -284,6 +284,13 @@ POLICY_PREFER_FFT = 16  # GSDR_POLICY_PREFER_FFT: int8 IQ on the FFT kernel even
 POLICY_I8_WS8 = 64  # GSDR_POLICY_I8_WS8: int8 decimating FIRs on the r04 8-way wave-specialised kernel
 
 
+def kernel_policy() -> int:
+    """The process-wide kernel-selection policy flags (gsdrAmdGetKernelPolicy)."""
+    L = lib()
+    L.gsdrAmdGetKernelPolicy.restype = ctypes.c_uint32
+    return int(L.gsdrAmdGetKernelPolicy())
+
+
 def set_kernel_policy(flags: int) -> int:
     """Set the process-wide kernel-selection policy; returns the previous flags."""
     L = lib()
