@@ -310,11 +310,16 @@ def kernel_compute(cls, n_out, T, D):
         s = (T + 62) // 32  # K-blocks of 32: K = 32 S >= T + 31
         return ("f16 MFMA (2 tap limbs, fp32 accumulate)", n_out * 2 * 2 * 32 * s * 2, F16_PEAK_TFLOPS)
     if cls == "i8-dec-mfma":
-        # r05 4-way kernel (fir_i8_ws4.hip): the smallest instantiated K quarter of 16-wide steps that
-        # covers 31 D + T (kW4KS), two f16 tap limbs, fp32 accumulate
+        # the 4-way kernel (fir_i8_ws4.hip, r05): the smallest instantiated K quarter of 16-wide steps that
+        # covers 31 D + T (kW4KS); the 8-way one (firI8WsKernel: GSDR_POLICY_I8_WS8, or no 4-way KS
+        # fits): 8 waves x ceil(K-steps / 8). Two f16 tap limbs, fp32 accumulate.
         ksteps = -(-(31 * D + T) // 16)
         need = -(-ksteps // 4)
-        k_pad = 4 * 16 * min(k for k in (2, 4, 6, 8, 11, 14, 17, 21, 22) if k >= need)
+        fits = [k for k in (2, 4, 6, 8, 11, 14, 17, 21, 22) if k >= need]
+        if i8_ws8_policy() or not fits:
+            k_pad = 8 * 16 * -(-ksteps // 8)
+        else:
+            k_pad = 4 * 16 * min(fits)
         return (f"f16 MFMA (split precision, 2 products, padded Toeplitz K = {k_pad}, fp32 accumulate)",
                 n_out * 2 * k_pad * 2 * 2, F16_PEAK_TFLOPS)
     if cls == "cf-mfma":
@@ -464,9 +469,23 @@ def cpu_baseline(wl, seconds_target=8.0):
     }
 
 
+KERNEL_POLICY = 0  # --kernel-policy (gsdrAmdSetKernelPolicy flags) of this run
+
+
+def i8_ws8_policy():
+    """The int8 decimating launches run on the 8-way kernel (GSDR_POLICY_I8_WS8 = 64)."""
+    return bool(KERNEL_POLICY & 64)
+
+
+def i8_dec_kernel(T, D):
+    """The wave-specialised int8 kernel a decimating launch of (T, D) runs on."""
+    need = -(-(-(-(31 * D + T) // 16)) // 4)
+    return "firI8WsKernel" if i8_ws8_policy() or need > 22 else "firI8Ws4Kernel"
+
+
 def kernel_name(chain):
     if isinstance(chain, AmChainSharded):
-        body = {"fft": "firFftKernel", "i8-dec-mfma": "firI8Ws4Kernel", "valu": "firLdsKernel"}.get(
+        body = {"fft": "firFftKernel", "i8-dec-mfma": i8_dec_kernel(chain.T, chain.D), "valu": "firLdsKernel"}.get(
             chain.kernel_class, chain.kernel_class)
         if chain.single:
             return (f"whole C5 step: gsdrInt8FirFCAmDemodFirFF ({body}<.., AUD>: RF FIR + AM + audio FIR in one "
@@ -479,7 +498,8 @@ def kernel_name(chain):
     entry = ("gsdrInt8FirFCAmDemodCarry" if chain.single else "gsdrInt8FirFCAmDemod") if chain.kind == "i8" \
         else "gsdrFirFCAmDemod"
     body = {"fft": "firFftD1PfKernel" if chain.D == 1 else "firFftKernel", "i8-mfma": "firI8MfmaKernel",
-            "i8-dec-mfma": "firI8Ws4Kernel", "cf-mfma": "firCfWsKernel", "valu": "firLdsKernel"}[chain.kernel_class]
+            "i8-dec-mfma": i8_dec_kernel(chain.T, chain.D), "cf-mfma": "firCfWsKernel",
+            "valu": "firLdsKernel"}[chain.kernel_class]
     return f"{entry} ({body})"
 
 
@@ -881,6 +901,8 @@ def main():
     stage = args.backend != "nccl"
     from gpusdr import ops
     if args.kernel_policy:
+        global KERNEL_POLICY
+        KERNEL_POLICY = args.kernel_policy
         ops.set_kernel_policy(args.kernel_policy)
     if args.workload == "c5":
         chain = (AmChainSharded(ops, rank, world, device, stage) if args.c5_mode == "sharded" else

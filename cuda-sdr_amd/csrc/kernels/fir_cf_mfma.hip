@@ -59,7 +59,7 @@ struct CfFirArgs {
   int32_t padShift;   // plane unit u lives at u + (u >> padShift)
   int32_t planeStride;  // bytes between the six planes (limb l, component c at 2 l + c)
   int32_t dbp;          // wave-specialised kernels: two partial-sum buffers
-  int32_t spinLimit;    // wave-specialised kernels: s_sleep iterations before a wait gives up
+  int32_t spinLimit;    // wave-specialised kernels: microseconds a hand-off wait may take before it gives up
   uint32_t* abortOut;   // wave-specialised kernels: host-visible abort counter (wsAbortWord)
 };
 
@@ -1044,7 +1044,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
       wsProducerTile<G>(a, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, wA);
       if (i + 2 >= n) break;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the wave
+    wsWaitWindow<0>(wA);  // no load outlives the wave, and none lands in a register reused meanwhile
+    wsWaitWindow<0>(wB);
     return;
   }
 
@@ -1299,6 +1300,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
       });
       if (i + 2 >= n) break;
     }
+    wsI8DrainWindows<G>(wA, wB);  // ws_common.h: no register reuse under a landing load
     if constexpr (AUD)
       for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile(a8, ring, c, t0, n, lead, t, ptid, ht, ab);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1534,6 +1536,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsGroupKernel(I8DecArgs a8
       });
       if (i + 2 >= n) break;
     }
+    wsI8DrainWindows<G>(wA, wB);
     if constexpr (AUD)
       for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) wsAudioTile<kGWaves>(a8, ring, c, t0, n, lead, t, ptid, ht, ab);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2213,8 +2216,8 @@ extern "C" __attribute__((visibility("default"))) hipError_t gsdrAmdWsDiag(unsig
 
 extern "C" {
 // include/gsdr/gsdr_amd.h: wave-specialised kernel hand-off limit and abort diagnostics.
-void gsdrAmdSetWsSpinLimit(int32_t iterations) {
-  gsdr_amd::gWsSpinLimit.store(iterations < 0 ? 0 : iterations, std::memory_order_relaxed);
+void gsdrAmdSetWsSpinLimit(int32_t microseconds) {
+  gsdr_amd::gWsSpinLimit.store(microseconds < 0 ? 0 : microseconds, std::memory_order_relaxed);
 }
 int32_t gsdrAmdGetWsSpinLimit(void) { return gsdr_amd::gWsSpinLimit.load(std::memory_order_relaxed); }
 

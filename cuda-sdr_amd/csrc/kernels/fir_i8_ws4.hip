@@ -505,6 +505,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
       if (i + 2 >= n) break;
     }
     (void)stp;
+    wsI8DrainWindows<G>(wA, wB);  // before the registers can go to the tail's code
     if constexpr (AUD)
       for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t)
         wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, t, ptid, ht, ab);

@@ -427,8 +427,9 @@ hipError_t gsdrAmChainStepHost(gsdrAmChain c, size_t slot, size_t* outputCount) 
   AMC_TRY(hipStreamWaitEvent(c->copyStream, c->readDone[p], 0));
   // the copies as kernels on the mapped pinned slots: hipMemcpyAsync here blocked the host thread for
   // 7-10 ms in 10 of ~600 calls (r05 HIP API trace: the DMA itself 0.18 ms, issued at the end of the call)
-  // (an odd r leaves the staging destination 2 bytes off dword alignment: the runtime copy then)
-  if (((2 * c->r) & 3) == 0)
+  // (the copy kernel moves whole dwords from dword-aligned addresses: an odd r leaves the staging
+  // destination 2 bytes off, an odd L the source slot and the byte count - the runtime copy then)
+  if ((((2 * c->r) | (2 * c->L)) & 3) == 0)
     AMC_TRY(gsdrAmdCopyKernel(c->staging[p] + 2 * c->r, c->hostInDev + 2 * c->L * slot, 2 * c->L, c->copyStream));
   else
     AMC_TRY(hipMemcpyAsync(c->staging[p] + 2 * c->r, c->hostIn + 2 * c->L * slot, 2 * c->L, hipMemcpyHostToDevice,

@@ -203,6 +203,18 @@ def hbm_probe(src: torch.Tensor, dst: torch.Tensor, mode: int) -> None:
           "gsdrAmdHbmProbe")
 
 
+def copy_kernel(dst: torch.Tensor, src: torch.Tensor) -> None:
+    """gsdrAmdCopyKernel on the current stream: src's bytes to dst by a copy kernel (dword-aligned
+    addresses and size; device or host-mapped memory)."""
+    n = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < n:
+        raise ValueError("dst too small")
+    L = lib()
+    L.gsdrAmdCopyKernel.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    dev = dst if dst.is_cuda else src
+    check(L.gsdrAmdCopyKernel(dst.data_ptr(), src.data_ptr(), n, _stream(dev)), "gsdrAmdCopyKernel")
+
+
 def quad_am_demod(z: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _require(z, torch.complex64, "z")
     if out is None:
@@ -331,14 +343,14 @@ def fir_kernel_class(x: torch.Tensor, taps: torch.Tensor, decimation: int, int8_
                                    x.data_ptr()).decode()
 
 
-def set_ws_spin_limit(iterations: int) -> int:
-    """Hand-off wait limit of the wave-specialised MFMA kernels (gsdrAmdSetWsSpinLimit, s_sleep
-    polls); returns the previous value."""
+def set_ws_spin_limit(microseconds: int) -> int:
+    """Hand-off wait budget of the wave-specialised MFMA kernels in microseconds of wall clock
+    (gsdrAmdSetWsSpinLimit; 0: give up at the first pending poll); returns the previous value."""
     L = lib()
     L.gsdrAmdGetWsSpinLimit.restype = ctypes.c_int32
     L.gsdrAmdSetWsSpinLimit.argtypes = [ctypes.c_int32]
     prev = L.gsdrAmdGetWsSpinLimit()
-    L.gsdrAmdSetWsSpinLimit(int(iterations))
+    L.gsdrAmdSetWsSpinLimit(int(microseconds))
     return prev
 
 

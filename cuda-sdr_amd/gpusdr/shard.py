@@ -251,37 +251,24 @@ class AmChainShard:
         g = self.geom
         return min(g.outputs, -(-g.head_rf // g.audio_decimation))
 
-    # r05 late: with the 4-way int8 kernel the multi-rank step faulted (hipErrorIllegalAddress, 2 and 8
-    # ranks at the bench's size) where the r04 8-way kernel runs: the bulk and head launches of
-    # a multi-rank step take the 8-way kernel until the fault is found
-    def _policy(self):
-        from . import ops
-        return ops.set_kernel_policy(ops.kernel_policy() | ops.POLICY_I8_WS8)
-
     def _bulk(self):
         """RF outputs [head_rf, rf_outputs) and, in the same launch, the audio outputs whose windows
-        lie in them (gsdrInt8FirFCAmDemodFirFF); the AM samples are kept for the head's audio."""
+        lie in them (gsdrInt8FirFCAmDemodFirFF); the AM samples are kept for the head's audio.
+        (r05 ran this launch and the head's on the 8-way kernel around a multi-rank fault of the 4-way
+        one; r06 found the cause - window loads landing in registers the compiler had already reused,
+        DESIGN.md 9 - and both run on the default kernel again.)"""
         from . import ops
         g = self.geom
         n_bulk = g.rf_outputs - g.head_rf
         ha = self.head_audio
-        prev = self._policy()
-        try:
-            ops.am_chain_fused(self.rf_taps, self.seg, g.decimation, n_bulk, self.am[g.head_rf:], 0, self.audio_taps,
-                               g.audio_decimation, g.outputs - ha, self.out[ha:], store_am=True)
-        finally:
-            ops.set_kernel_policy(prev)
+        ops.am_chain_fused(self.rf_taps, self.seg, g.decimation, n_bulk, self.am[g.head_rf:], 0, self.audio_taps,
+                           g.audio_decimation, g.outputs - ha, self.out[ha:], store_am=True)
 
     def _head(self):
         """RF outputs [0, head_rf) (they read the halo), then the audio outputs that read them."""
         from . import ops
         g = self.geom
-        prev = self._policy()
-        try:
-            ops.fir(self.rf_taps, self.buf, g.decimation, g.head_rf, out=self.am[: g.head_rf], am=True,
-                    int8_iq=True)
-        finally:
-            ops.set_kernel_policy(prev)
+        ops.fir(self.rf_taps, self.buf, g.decimation, g.head_rf, out=self.am[: g.head_rf], am=True, int8_iq=True)
         ha = self.head_audio
         if ha > 0:
             ops.fir(self.audio_taps, self.am, g.audio_decimation, ha, out=self.out[:ha])

@@ -166,12 +166,14 @@ GSDR_API float gsdrAmdGetFftGuard(void);
  * (synchronises the device; reset != 0 zeroes the counter). */
 GSDR_API hipError_t gsdrAmdFftDirectBlocks(int32_t device, uint64_t* count, int reset);
 /* Wave-specialised (producer / consumer) MFMA FIR kernels: every hand-off wait gives up after
- * `iterations` s_sleep(1) polls (default 1 << 22, ~0.1 s), releases all other waits so the grid
- * drains, and counts the abort in a host-visible word. Such a launch's outputs are undefined; the
+ * `microseconds` of wall clock (s_memrealtime; default 2 000 000 = 2 s; 0: at the first poll that finds
+ * the hand-off pending - tests), releases all other waits so the grid drains, and counts the abort in a
+ * host-visible word. (Through r05 the limit counted s_sleep polls, whose duration depends on whatever
+ * else runs on the CU.) Such a launch's outputs are undefined; the
  * next gsdr* call that launches a wave-specialised kernel on that device returns
  * hipErrorLaunchTimeOut (and clears the count). gsdrAmdWsAborts synchronises `device` and reads
  * the count (reset != 0 clears it). */
-GSDR_API void gsdrAmdSetWsSpinLimit(int32_t iterations);
+GSDR_API void gsdrAmdSetWsSpinLimit(int32_t microseconds);
 GSDR_API int32_t gsdrAmdGetWsSpinLimit(void);
 GSDR_API hipError_t gsdrAmdWsAborts(int32_t device, uint64_t* count, int reset);
 /* The count is per DEVICE, not per stream or executor: an abort raised by a launch of another stream
@@ -187,6 +189,8 @@ GSDR_API uint32_t gsdrAmdWsAbortsPending(int32_t device);
  * (tools/source_hash.py: kernels, runtime, C API, public headers, Makefile). A library that does not
  * match the tree it is tested with fails tests/test_abi_exports.py. */
 GSDR_API const char* gsdrAmdBuildId(void);
+/* The compiler that built it: HIP and clang version numbers (not part of the id, r06). */
+GSDR_API const char* gsdrAmdBuildCompiler(void);
 /* Diagnostics: HBM bandwidth probe over `bytes` (16-byte aligned device buffers): mode 0 streams
  * `input` (float4 loads, one sum per thread; `output` untouched for finite data), mode 1 copies it to
  * `output`. The bench times it to report the roofline against measured bandwidth as well as spec. */

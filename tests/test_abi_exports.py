@@ -123,6 +123,21 @@ def test_build_id_folds_in_compile_flags():
     assert "--extra-flags='$(EXTRA_FLAGS)'" in mk and "$(FLAGSTAMP)" in mk
 
 
+def test_build_id_independent_of_compiler_location(built, tmp_path):
+    """the id does not depend on the checking machine's compiler (a missing hipcc, or ROCm
+    installed elsewhere, gave another id for the same sources); the compiler's version numbers are embedded
+    beside it (gsdrAmdBuildCompiler) without install paths."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import source_hash as sh
+    assert sh.compiler_version(str(tmp_path / "no-such-hipcc")) == ""
+    assert "/" not in sh.compiler_version()
+    code = ("import ctypes,sys; L=ctypes.CDLL(sys.argv[1]); f=L.gsdrAmdBuildCompiler; "
+            "f.restype=ctypes.c_char_p; print(f().decode())")
+    r = subprocess.run([sys.executable, "-c", code, built], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == sh.compiler_version()
+
+
 @pytest.mark.gpu
 def test_gpu_box_library_matches_source_tree():
     """The same check where the GPU suite runs: the pushed, prebuilt .so the box loads must be the one
