@@ -65,15 +65,19 @@ def test_am_chain_device_steps(chain_mod, orc, T, D, Ta, Da, L, poison):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("poison", [False, True])
-def test_am_chain_host_ring_matches_device(chain_mod, orc, poison):
+@pytest.mark.parametrize("T,Da,L,poison", [(255, 8, 8000, False), (255, 8, 8000, True),
+                                           (258, 8, 8000, False), (258, 3, 7995, False), (255, 3, 7995, False)])
+def test_am_chain_host_ring_matches_device(chain_mod, orc, T, Da, L, poison):
     """Pinned-ring steps (H2D on a second stream, double-buffered staging) give bit-identical
     output to the device-input steps; reset() starts a fresh stream. `poison`: LDS filled with NaN on
     the chain's stream before every pinned-ring step (r04's one bitwise mismatch of
-    this test was never shown to be the stale-LDS defect)."""
+    this test was never shown to be the stale-LDS defect). The RF history r (the next multiple of D at or
+    above T - 1) and the chunk L odd and even: the copy kernel moves the chunk only when
+    2 r and 2 L are whole dwords (T = 258, L = 8 000); an odd r (255) or an odd L (7 995) takes the
+    runtime copy."""
     import torch
     from gpusdr import ops
-    T, D, Ta, Da, L = 255, 5, 63, 8, 8000
+    D, Ta = 5, 63
     rng = np.random.default_rng(5)
     rf = orc.lowpass_taps(T, 0.08)
     au = orc.lowpass_taps(Ta, 0.05)

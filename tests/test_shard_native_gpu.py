@@ -213,3 +213,49 @@ def test_native_shard_stream_rejects_bad_shapes():
         ShardStream(0, 1, np.ones(8, np.float32), 3, 1000)  # L not a multiple of D
     with pytest.raises(RuntimeError):
         ShardStream(0, 2, np.ones(8, np.float32), 1, 1000)  # two ranks need an exchange
+
+
+def test_native_shard_stream_failed_exchange_then_destroy(orc):
+    """the failure paths of the executor. A world-1 stream whose exchange hook fails on its
+    second step: that step reports the error (the bulk launch already enqueued, no head), destroy() then
+    returns with nothing of the executor left pending (it waits on the events of the steps that did run),
+    the device is healthy, and a fresh executor over the same stream positions matches the float64 oracle."""
+    import torch
+
+    from gpusdr import ops
+    from gpusdr._native import HipError
+    from gpusdr.native_shard import ShardStream
+
+    i8, am, T, D, L = CASES["c3"]
+    dev = torch.device("cuda", 0)
+    taps = orc.lowpass_taps(T, 0.04, "blackman")
+    H = T - 1
+    calls = []
+
+    def flaky(send_tail, recv_halo, nbytes, next_rank, prev_rank, xstream):
+        calls.append(1)
+        if len(calls) == 2:
+            raise RuntimeError("injected exchange failure")
+
+    s = ShardStream(0, 1, taps, D, L, int8_iq=i8, am=am, exchange=flaky)
+    s.write_halo(_stream_piece(ops, torch, i8, 0, H, dev))
+    s.write_segment(_stream_piece(ops, torch, i8, H, L, dev))
+    s.step()
+    s.write_segment(_stream_piece(ops, torch, i8, H + L, L, dev))
+    with pytest.raises(HipError):
+        s.step()
+    s.close()
+    torch.cuda.synchronize()  # nothing of the executor failed the device
+    # a fresh executor: the stream from its start, checked against float64
+    s = ShardStream(0, 1, taps, D, L, int8_iq=i8, am=am, exchange=lambda *a: None)
+    s.write_halo(_stream_piece(ops, torch, i8, 0, H, dev))
+    outs = []
+    for step in range(2):
+        s.write_segment(_stream_piece(ops, torch, i8, H + step * L, L, dev))
+        outs.append(s.step().cpu().numpy().copy())
+    s.close()
+    got = np.concatenate(outs)
+    x = _stream_piece(ops, torch, i8, 0, H + 2 * L, dev).cpu().numpy()
+    y64, bound = orc.fir_f64(taps, x, D, 2 * L // D)
+    err = np.abs(got.astype(np.complex128) - np.abs(y64))
+    assert np.all(err <= FIR_TOL * bound + 1e-30), float(np.max(err / (bound + 1e-30)))
