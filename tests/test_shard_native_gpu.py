@@ -247,7 +247,7 @@ def test_native_shard_stream_failed_exchange_then_destroy(orc):
     s.close()
     torch.cuda.synchronize()  # nothing of the executor failed the device
     # a fresh executor: the stream from its start, checked against float64
-    s = ShardStream(0, 1, taps, D, L, int8_iq=i8, am=am, exchange=lambda *a: None)
+    s = ShardStream(0, 1, taps, D, L, int8_iq=i8, am=am)  # world 1 without a hook: the history carry
     s.write_halo(_stream_piece(ops, torch, i8, 0, H, dev))
     outs = []
     for step in range(2):
