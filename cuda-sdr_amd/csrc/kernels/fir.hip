@@ -732,6 +732,9 @@ FirPlanShape planFirShape(size_t tapCount, size_t decimation) {
   return s;
 }
 
+// cf32 decimating FC launches below this many input samples take the MFMA kernel, not the FFT (launchFir)
+constexpr uint64_t kFftMinCf32Samples = uint64_t{1} << 24;
+
 struct MixSpec {
   bool on = false;
   uint64_t phase0 = 0, step = 0;
@@ -757,7 +760,16 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
   // frequency shifter folded into it when mixing (row chirp on the loaded rows, the per-phase factor
   // in the filter spectra, the block's factor on the outputs)
   if constexpr (MODE == kFirFC && (INK == kInI8IQ || INK == kInCF32) && EPI != kEpiPair && EPI != kEpiFm) {
-    if ((kernelPolicy() & (GSDR_POLICY_NO_FFT | GSDR_POLICY_NO_MFMA)) == 0 &&
+    // Small decimating cf32 launches (below ~2^24 input samples: a live stream's 2^22-sample steps) go to
+    // the split-precision MFMA kernel: the FFT kernel builds its filter spectra per workgroup and hands
+    // out one 5 120-sample block per wave per round, so a 2^22-sample launch fills 40 % of one round and
+    // pays the whole prologue (r06 probe, C3's filter: 2^22 samples FFT 24.3 us vs MFMA 19.9 us per launch;
+    // 2^24 44-49 vs 46-50; 2^26 136-144 vs 153-157 - profiles/r06/c3_stream_probe.log)
+    const bool smallCf = INK == kInCF32 && !mix.on && decimation >= 2 &&
+                         (uint64_t)nOut * decimation < kFftMinCf32Samples &&
+                         (kernelPolicy() & (GSDR_POLICY_NO_MFMA | GSDR_POLICY_PREFER_FFT)) == 0 &&
+                         firCfMfmaEligible(tapCount, decimation, in);
+    if (!smallCf && (kernelPolicy() & (GSDR_POLICY_NO_FFT | GSDR_POLICY_NO_MFMA)) == 0 &&
         firFftEligible(tapCount, decimation, in, INK == kInI8IQ, mix.on))
       return launchFirFft(in, INK == kInI8IQ, taps, tapCount, decimation, out, nOut, EPI, stream,
                           FftMix{mix.on, mix.phase0, mix.step});

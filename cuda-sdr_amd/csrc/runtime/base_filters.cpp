@@ -1,7 +1,5 @@
 // BaseSink / BaseSource / BaseFilter (reference src/filters/BaseSink.cpp:25-178,
 // BaseSource.cpp:19-22, BaseFilter.cpp:21-28), with lazy compaction of the input window.
-#include <algorithm>
-
 #include <gpusdrpipeline/abi/base_filters.h>
 #include <gpusdrpipeline/abi/errors.h>
 
@@ -51,15 +49,11 @@ Result<IBuffer> BaseSink::requestBuffer(size_t port, size_t numBytes) noexcept {
   IRelocatableResizableBuffer* b = p.inputBuffer.get();
   IBufferRange* r = b->range();
   if (r->remaining() < numBytes) {
-    // The window is sized so that compaction (one D2D copy of the retained history, a ~5 us launch
-    // however small the history) runs once per several steps, not per step: at least 2x what this
-    // request needs, and up to 8x while that adds no more than 256 MiB (r06: at 2^22-sample cf32
-    // pushes - the C3 stream - a 2x window compacted on every push, 4.8 us of each 38 us step).
-    // Retired bytes in front are reclaimed before the window grows.
-    const size_t need = r->used() + numBytes;
-    const size_t target = std::max(2 * need, std::min(8 * need, need + (size_t{256} << 20)));
+    // retired bytes in front of the window are reclaimed first (one small D2D copy of the
+    // retained history), and only then does the window grow - with 2x headroom so the next
+    // steps append without compacting
     if (r->offset() != 0) FWD_IN_RESULT_IF_ERR(b->relocateUsedToStart());
-    if (r->capacity() < target) FWD_IN_RESULT_IF_ERR(b->resize(target));
+    if (r->remaining() < numBytes) FWD_IN_RESULT_IF_ERR(b->resize(2 * (r->endOffset() + numBytes)));
   }
   p.bufferCheckedOut = true;
   Result<IBuffer> lent = mSlicedBufferFactory->sliceRemaining(b);

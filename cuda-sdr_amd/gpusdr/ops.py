@@ -292,7 +292,7 @@ POLICY_NO_MFMA = 1  # include/gsdr/gsdr_amd.h GSDR_POLICY_NO_MFMA
 POLICY_CF_BF16 = 2  # GSDR_POLICY_CF_BF16
 POLICY_NO_WS = 4  # GSDR_POLICY_NO_WS: barrier-synchronous decimating MFMA kernels
 POLICY_NO_FFT = 8  # GSDR_POLICY_NO_FFT: long real-tap FIRs on the direct forms, not the FFT kernel
-POLICY_PREFER_FFT = 16  # GSDR_POLICY_PREFER_FFT: int8 IQ on the FFT kernel even where int8 MFMA applies
+POLICY_PREFER_FFT = 16  # GSDR_POLICY_PREFER_FFT: the FFT kernel wherever eligible (int8 IQ, small cf32 launches)
 POLICY_I8_WS8 = 64  # GSDR_POLICY_I8_WS8: int8 decimating FIRs on the r04 8-way wave-specialised kernel
 
 

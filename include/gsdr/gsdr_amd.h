@@ -144,8 +144,10 @@ GSDR_API hipError_t gsdrFmDemod(size_t rfSampleRate, float tunedFrequency, float
 /* Long real-tap FIRs (T >= 256, D in {2,4,6,8,10}) on the matrix-core / VALU direct forms instead of
  * the FFT fast convolution (polyphase overlap-save, fp32). */
 #define GSDR_POLICY_NO_FFT 8u
-/* int8 IQ input takes the FFT fast convolution even where the int8 MFMA kernels apply (by default
- * they do: faster for int8 at the C5 shape); A/B comparisons and tests of the int8 FFT path. */
+/* The FFT fast convolution wherever it is eligible: int8 IQ input even where the int8 MFMA kernels
+ * apply (by default they do: faster for int8 at the C5 shape), and cf32 launches below 2^24 input
+ * samples, which by default take the MFMA kernel (r06: faster for a live stream's small steps); A/B
+ * comparisons and tests of the FFT path at small sizes. */
 #define GSDR_POLICY_PREFER_FFT 16u
 /* int8 IQ decimating MFMA FIRs (and the fused C5 chain) on the 8-way split-K wave-specialised kernel of
  * r01-r04 instead of the 4-way one (r05: one consumer wave per SIMD); A/B

@@ -135,7 +135,8 @@ def test_fft_fir_large_stream_properties(ops, orc):
     x_d = ops.synth_wideband_cf32(0xC3, 0.013, 0.31, 0, n_in)
     taps = orc.lowpass_taps(T, 0.04, "blackman")
     taps_d = _dev(taps)
-    am = _host(ops.fir(taps_d, x_d, D, n_out, am=True))
+    with _Policy(ops, ops.POLICY_PREFER_FFT):  # below 2^24 input samples cf32 takes the MFMA kernel by default
+        am = _host(ops.fir(taps_d, x_d, D, n_out, am=True))
     x = _host(x_d)
     rng = np.random.default_rng(3)
     ks = np.unique(np.concatenate([rng.integers(0, n_out, 3000), [0, n_out - 1]]))
@@ -287,7 +288,8 @@ def test_fft_fir_guard_zero_is_direct(ops, orc, D, per_block):
     prev = ops.set_fft_guard(0.0)
     try:
         ops.fft_direct_blocks(reset=True)
-        y = _host(ops.fir(_dev(taps), _dev(x), D, n_out))
+        with _Policy(ops, ops.POLICY_PREFER_FFT):
+            y = _host(ops.fir(_dev(taps), _dev(x), D, n_out))
         direct = ops.fft_direct_blocks(reset=True)
     finally:
         ops.set_fft_guard(prev)
