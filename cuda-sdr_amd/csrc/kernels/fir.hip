@@ -732,7 +732,15 @@ FirPlanShape planFirShape(size_t tapCount, size_t decimation) {
   return s;
 }
 
-// cf32 decimating FC launches below this many input samples take the MFMA kernel, not the FFT (launchFir)
+// cf32 decimating FC launches below this many input samples take the MFMA kernel, not the FFT (launchFir):
+// OFF (r06). The routing made a live stream's 2^22-sample steps 17 % faster (C3 stream 111 -> 132 Gs/s), but the
+// FFT kernel's adversarial tests (silence, impulses, a non-finite sample: tests/test_fft_fir.py) then ran on
+// the MFMA kernel and failed there - its per-tile guard does not cover exact-zero blocks, and the f16 x 2 taps
+// drop the Blackman tails. Kept switchable until that kernel's guard is complete.
+#ifndef GSDR_FFT_SMALL_TO_MFMA
+#define GSDR_FFT_SMALL_TO_MFMA 0
+#endif
+constexpr bool kFftSmallToMfma = GSDR_FFT_SMALL_TO_MFMA != 0;
 constexpr uint64_t kFftMinCf32Samples = uint64_t{1} << 24;
 
 struct MixSpec {
@@ -765,7 +773,7 @@ hipError_t launchFir(const void* in, const float* taps, size_t tapCount, size_t 
     // out one 5 120-sample block per wave per round, so a 2^22-sample launch fills 40 % of one round and
     // pays the whole prologue (r06 probe, C3's filter: 2^22 samples FFT 24.3 us vs MFMA 19.9 us per launch;
     // 2^24 44-49 vs 46-50; 2^26 136-144 vs 153-157 - profiles/r06/c3_stream_probe.log)
-    const bool smallCf = INK == kInCF32 && !mix.on && decimation >= 2 &&
+    const bool smallCf = kFftSmallToMfma && INK == kInCF32 && !mix.on && decimation >= 2 &&
                          (uint64_t)nOut * decimation < kFftMinCf32Samples &&
                          (kernelPolicy() & (GSDR_POLICY_NO_MFMA | GSDR_POLICY_PREFER_FFT)) == 0 &&
                          firCfMfmaEligible(tapCount, decimation, in);
