@@ -808,6 +808,10 @@ __device__ __forceinline__ void wsReduceFinish(const CfFirArgs& a, WsCtl* c, int
     wsSignal(&c->partsFree[b], lane);
     const int orow = (wave & 3) + 8 * (wave >> 2) + 4 * (lane >> 5);
     const int64_t k = (int64_t)tile * kCfTileOut + 32 * orow + (lane & 31);
+    // int8: the zero-window guard's tiles (mode bit 1, ws_common.h wsI8ZeroRun) in the direct fp32 form;
+    // a.x carries the int8 input (iq4 + sub) on the int8 path
+    if (I8 && (mode & 1) && k < a.nOut)
+      wsI8DirectOutput(reinterpret_cast<const int8_t*>(a.x), a.taps, a.T, a.D, k, sh, yi, yq);
     if constexpr (AUD) {  // int8, AM: the tile's AM samples into the ring for the producers' audio FIR
       const float v = __builtin_amdgcn_sqrtf(fmaf(yi, yi, yq * yq)) * ldexpf(1.0f / 127.0f, -sh);
       // slot j mod kAmRing is free once the producers finished the audio outputs of tile j - kAmRing + 1
@@ -878,7 +882,8 @@ __device__ __forceinline__ void wsConsumers(const CfFirArgs& a, int8_t* smem, fl
     const int set = i & 1;
     const int tile = t0 + i;
     wsWait(c, &c->planesFull[set], kWsProducers * ((i >> 1) + 1));
-    const int mode = waveUniform(c->mode[set]);
+    // int8: bit 0 = the zero-window guard's flag (the cf32 kernels: the tile's scale, or kWsDirect)
+    const int mode = I8 ? (wsI8Zflag(c, set) ? 1 : 0) : waveUniform(c->mode[set]);
     if (!I8 && mode == kWsDirect) {
       wsSignal(&c->planesFree[set], lane);
       directTile<EPI>(a, tile, tid);
@@ -1310,6 +1315,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firI8WsKernel(I8DecArgs a8, int
     return;
   }
   CfFirArgs a{};
+  a.x = reinterpret_cast<const float*>(a8.iq4 + a8.sub);  // the int8 input (the zero-window guard's direct form)
   a.taps = a8.taps;
   a.out = a8.out;
   a.nOut = a8.nOut;

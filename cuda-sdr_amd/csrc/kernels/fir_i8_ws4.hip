@@ -148,6 +148,20 @@ __device__ __forceinline__ void w4RingWrite(float* ring, int j, int tid, const f
   }
 }
 
+// The zero-window guard's tiles (ws_common.h wsI8ZeroRun): this lane's two outputs of tile `tile` in the
+// direct fp32 form, as the sums w4Outputs takes {yi0, yi1, yq0, yq1}.
+__device__ __forceinline__ f4 w4DirectY(const I8DecArgs& a, int tile, int tid, int sh) {
+  const int lane = tid & (kWave - 1);
+  const int wave = tid >> 6;
+  float yi[2] = {0.0f, 0.0f}, yq[2] = {0.0f, 0.0f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t k = (int64_t)tile * kCfTileOut + 32 * (wave + 8 * h + 4 * (lane >> 5)) + (lane & 31);
+    if (k < a.nOut) wsI8DirectOutput(a.iq4 + a.sub, a.taps, a.T, a.D, k, sh, yi[h], yq[h]);
+  }
+  return f4{yi[0], yi[1], yq[0], yq[1]};
+}
+
 __device__ __forceinline__ void w4AmFreeWait(WsCtl* c, int j) {  // ring slot of tile j reusable
   if (j - kAmRing + 2 > 0) wsWait(c, &c->amFree, kWsProducers * (j - kAmRing + 2));
 }
@@ -239,6 +253,7 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
   const int uRow = (kW4Q8 ? 2 : 4) * D * arow + half;  // A row arow: 32 D samples = 2 D int8 / 4 D f16 slots
   const float outScale = ldexpf(1.0f / 127.0f, -sh);
   float am[2] = {0.0f, 0.0f};  // AUD: AM samples of tile i - 2 (this lane's), written to the ring in tile i's loop
+  bool zPrev = false, zCur = false;  // zero-window guard: tiles i - 1 and i take the direct form
 #ifdef GSDR_W4_STAMPS
   unsigned long long cst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tlast = __builtin_amdgcn_s_memtime();
@@ -270,6 +285,8 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
 #ifdef GSDR_W4_STAMPS
     if (wave == 0) { W4TR(0, i, 0) }
 #endif
+    zPrev = zCur;
+    zCur = wsI8Zflag(c, set);  // read before this tile's planesFree lets the producers rewrite it
     const int8_t* pI = smem + set * 2 * a.planeStride + comp * a.planeStride;
 #if GSDR_W4_Q8
     v16i acc0 = v16i{}, acc1 = v16i{}, acc2 = v16i{};
@@ -346,6 +363,7 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
       if (!(GSDR_WS_ABL & 2)) pb[(wave * 4 + r) * kWave + lane] = f4{acc[r], acc[r + 4], acc[r + 8], acc[r + 12]};
       else asm volatile("" ::"v"(acc[r]), "v"(acc[r + 4]), "v"(acc[r + 8]), "v"(acc[r + 12]));
 #if GSDR_W4_LATESIG  // the previous tile's outputs while the partial writes land
+    if (red && zPrev) y = w4DirectY(a, t0 + i - 1, tid, sh);
     if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am);
     W4ST(6)
     if (GSDR_W4_NOFENCE) {
@@ -358,6 +376,7 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
 #else
     wsSignal(&c->partsFull[b], lane);
     W4ST(5)
+    if (red && zPrev) y = w4DirectY(a, t0 + i - 1, tid, sh);
     if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am);
     W4ST(6)
 #endif
@@ -379,6 +398,7 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
 #pragma unroll
     for (int v = 0; v < kW4Consumers; ++v) y += *w4Part(part, rb, v, wave, lane);
     wsSignal(&c->partsFree[rb], lane);
+    if (zCur) y = w4DirectY(a, t0 + j, tid, sh);
     w4Outputs<EPI, AUD>(a, outScale, t0 + j, j, tid, y, lead, am);
     if constexpr (AUD) {
       w4AmFreeWait(c, j);

@@ -88,6 +88,8 @@ struct WsCtl {
   int mode[3];                        // per plane set: scale exponent sx, or kWsDirect
   float stat[2][2][kWsProducers];     // [tile parity][max, smallest block max][producer wave]
   int amSlot[kAmRing];                // fused audio stage: consumer waves' AM signals per ring slot
+  int zflag[3][kWsProducers];         // int8 kernels, per plane set and producer wave: the tile's window holds an
+                                      // exact-zero run (wsI8ZeroRun) - the consumers compute it in the direct form
   // set once by thread 0 (not part of the zeroed hand-off words above)
   int spinLimit;  // hand-off wait budget, microseconds
   uint32_t* abortOut;
@@ -332,6 +334,49 @@ __device__ __forceinline__ void wsI8DrainWindows(I8WsWindow<G>& a, I8WsWindow<G>
   }
 }
 
+// The zero-window guard of the int8 kernels (r06). The taps are two f16 limbs under one
+// block scale: a tap below ~2^-17 of the largest keeps only an absolute 2^-39 of it (the Blackman tails of
+// C5's RF filter: 1e-20 .. 1e-8 of the largest), so an output whose window has non-zero samples ONLY under
+// such taps - at a zero-padded stream start, after an exact-zero gap - misses the 1e-6 sum|h||x| bound.
+// Such a window's samples under every other tap are zero, i.e. the tile window holds a long run of exact
+// complex zeros. A wave flags its part of the window when two consecutive 8-sample units of its 64 are all
+// zero (I = Q = 0; units past Wl excluded): any zero run of >= 31 samples is caught (>= 3 whole units, two
+// of them in one wave's 64), and the violating runs are ~T long. Flagged tiles are computed in the direct
+// fp32 form by the consumers (wsI8DirectOutput). An adversarial comb - non-zero samples only where a
+// windowed sinc has its zeros - is not a run and stays uncaught. Cost: 3 VALU per unit.
+__device__ __forceinline__ bool wsI8ZeroRun(const uint32_t (&words)[4], bool valid) {
+  const uint32_t o = words[0] | words[1] | words[2] | words[3];
+  const uint64_t zm = __ballot(valid && o == 0u);
+  return (zm & (zm >> 1)) != 0;
+}
+
+// zero-window flags of plane set `set` (the producer waves' zflag words, read after planesFull)
+__device__ __forceinline__ bool wsI8Zflag(const WsCtl* c, int set) {
+  return waveUniform(c->zflag[set][0] | c->zflag[set][1] | c->zflag[set][2] | c->zflag[set][3]) != 0;
+}
+
+// Direct fp32 form of int8 IQ output k (the guard's tiles): {sum_j h_j I'_kD+j, sum_j h_j Q'_kD+j} with
+// x' = max(x, -127), 64-tap blocked partial sums (the VALU kernels' order class), in the MFMA path's
+// scaled units (x 2^sh) so the caller's epilogue (x 2^-sh / 127) applies unchanged.
+__device__ __forceinline__ void wsI8DirectOutput(const int8_t* iq, const float* taps, int T, int D, int64_t k, int sh,
+                                                 float& yi, float& yq) {
+  const int8_t* p = iq + 2 * k * D;
+  float si = 0.0f, sq = 0.0f;
+  for (int j0 = 0; j0 < T; j0 += 64) {
+    const int j1 = T < j0 + 64 ? T : j0 + 64;
+    float pi = 0.0f, pq = 0.0f;
+    for (int j = j0; j < j1; ++j) {
+      const float h = taps[j];
+      pi = fmaf(h, (float)max((int)p[2 * j], -127), pi);
+      pq = fmaf(h, (float)max((int)p[2 * j + 1], -127), pq);
+    }
+    si += pi;
+    sq += pq;
+  }
+  yi = ldexpf(si, sh);
+  yq = ldexpf(sq, sh);
+}
+
 // Producer, tile i: wCur holds tile i's window (complete after the wait), wNext tile i + 1's.
 // `pre` runs while the window is still landing (the fused audio stage hides its work under that
 // wait; its few output stores sit behind tile i + 1's loads in the vmcnt order - issued a tile
@@ -377,6 +422,7 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 #endif
   int8_t* planes = smem + set * 2 * a.planeStride;
   const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
+  bool zrun = false;
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     const int g = ptid + kWsPThreads * j;
@@ -384,6 +430,7 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
                                __builtin_amdgcn_alignbyte(wCur.q[j].z, wCur.q[j].y, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.q[j].w, wCur.q[j].z, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.e[j], wCur.q[j].w, a.sub)};
+    zrun |= wsI8ZeroRun(words, g < Wl);
     if constexpr (Q8) {
       uint2 iu, qu;
       int8IqToI8Units(words, iu, qu);
@@ -415,6 +462,7 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
     wsI8LoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
   }
   if (ptid == 0) c->mode[set] = 0;
+  if (lane == 0) c->zflag[set][ptid >> 6] = zrun ? 1 : 0;  // published by the planesFull release
   wsSignal(&c->planesFull[set], lane);
 #if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
   if (st) st[3] += __builtin_amdgcn_s_memtime() - t0s;
