@@ -86,15 +86,18 @@ struct WsCtl {
   int amFree;                         // producer waves done with the audio outputs of a tile
   int abort;
   int mode[3];                        // per plane set: scale exponent sx, or kWsDirect
-  float stat[2][2][kWsProducers];     // [tile parity][max, smallest block max][producer wave]
+  union {                             // (the static LDS budget: kCfDynLdsMax leaves 256 bytes)
+    float stat[2][2][kWsProducers];   // cf32: [tile parity][max, smallest block max][producer wave]
+    int zflag[4][kWsProducers];       // int8, per plane set and producer wave: the tile's window holds an exact-
+                                      // zero run (wsI8ZeroRun) - the consumers compute it in the direct form
+  };
   int amSlot[kAmRing];                // fused audio stage: consumer waves' AM signals per ring slot
-  int zflag[3][kWsProducers];         // int8 kernels, per plane set and producer wave: the tile's window holds an
-                                      // exact-zero run (wsI8ZeroRun) - the consumers compute it in the direct form
   // set once by thread 0 (not part of the zeroed hand-off words above)
   int spinLimit;  // hand-off wait budget, microseconds
   uint32_t* abortOut;
 };
 constexpr int kWsCtlZeroWords = (int)(offsetof(WsCtl, spinLimit) / 4);
+static_assert(sizeof(WsCtl) + 12 * sizeof(float) <= 256, "WsCtl + waveMax must fit the 256 static LDS bytes");
 
 // Diagnostic builds only (-DGSDR_WS_DIAG=1: tools/build_variant.sh diag, run by tools/r05/session.sh diag; the product build has none): bounds
 // checks on every index the fused audio stage and the AM ring writes compute, counted per kind, to
