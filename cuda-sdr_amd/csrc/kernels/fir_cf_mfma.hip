@@ -136,16 +136,25 @@ __device__ __forceinline__ void splitWindow(const CfFirArgs& a, const CfWindow<G
   if (pr != pr) *nonFinite = 1;
 }
 
-// Direct fp32 form of one tile, one output per thread (tiles holding a non-finite sample).
+// Direct fp32 form of one tile, one output per thread (the statistics' tiles: a non-finite sample, a quiet
+// or exact-zero 64-sample block).
 template <int EPI>
 __device__ __forceinline__ void directTile(const CfFirArgs& a, int tile, int tid) {
   const int64_t k = (int64_t)tile * kCfTileOut + tid;
   if (k >= a.nOut) return;
   const f2* x = reinterpret_cast<const f2*>(a.x) + k * a.D;
-  f2 y = f2{0.0f, 0.0f};
-  for (int j = 0; j < a.T; ++j) y += a.taps[j] * x[j];
-  if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = amEnvelope(y);
-  else reinterpret_cast<f2*>(a.out)[k] = y;
+  // accumulated in double (rare tiles: the sequential fp32 sum of ~1 000 products reached 1.2e-6 of
+  // sum|h||x| - tests/test_mfma_guard.py), then the envelope in double too: the guard's tiles hold outputs
+  // far below 1 (windows whose samples meet only tail taps), whose squares would be fp32 subnormals
+  double yr = 0.0, yi = 0.0;
+  for (int j = 0; j < a.T; ++j) {
+    const double h = a.taps[j];
+    const f2 v = x[j];
+    yr = fma(h, (double)v.x, yr);
+    yi = fma(h, (double)v.y, yi);
+  }
+  if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = (float)__builtin_sqrt(fma(yr, yr, yi * yi));
+  else reinterpret_cast<f2*>(a.out)[k] = f2{(float)yr, (float)yi};
 }
 
 template <int KS, int G, int EPI>
@@ -280,17 +289,35 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfMfmaKernel(CfFirArgs a) {
 // direct fp32 path, so every output keeps its error relative to its OWN window
 // (test_cf_mfma_dynamic_range).
 
+// Window units (8 samples) of tile `tile` wholly inside the input, capped at the units loaded (`cap`).
+__device__ __forceinline__ int cfUnitsInInput(const CfFirArgs& a, int tile, int cap) {
+  const int64_t u = (a.nIn - (int64_t)tile * kCfTileOut * a.D) >> 3;
+  return u < cap ? (int)(u > 0 ? u : 0) : cap;
+}
+
+// The exact-zero rule (r06): the taps are two f16 limbs under one block scale, so a
+// tap below ~2^-17 of the largest keeps only an absolute 2^-39 of it (a Blackman filter's tails), and an
+// output whose window has non-zero samples ONLY under such taps - after an exact-zero gap, at a
+// zero-padded start, between sparse impulses - misses the 1e-6 sum|h||x| bound. Such a window holds
+// long exact-zero runs, i.e. whole zero 64-sample blocks: a block wholly inside the input counts in the
+// smallest-block statistic even when it is zero, which sends the tile to the direct path (B = 0 < M /
+// 2^16). The blocks of the last tile past the input's end do not count. Unit g's block: lanes g & ~7 ..
+// g | 7 (g = lane mod 8: the thread strides are multiples of 64).
+__device__ __forceinline__ bool cfBlockInInput(int g, int inU) { return (g | 7) < inU; }
+
 // Window statistics of one tile, in two halves around a barrier the caller provides:
 // cfStatsLocal reduces the thread's units over the wave and leaves the wave's (max, smallest
 // nonzero 64-sample-block max) in red[.][wave]; cfStatsFinish reads all waves' after the barrier
 // and decides the tile's scale or the direct path.
 template <int G>
-__device__ __forceinline__ void cfStatsLocal(const CfFirArgs& a, const CfWindow<G>& w, int tid, float (*red)[kCfWaves]) {
+__device__ __forceinline__ void cfStatsLocal(const CfFirArgs& a, const CfWindow<G>& w, int tile, int tid,
+                                             float (*red)[kCfWaves]) {
   const int lane = tid & (kWave - 1);
   const int wave = tid >> 6;
   float m = 0.0f;         // largest |component| of this thread's units
-  float bmin = INFINITY;  // smallest nonzero 64-sample-block maximum seen by this thread
+  float bmin = INFINITY;  // smallest 64-sample-block maximum seen by this thread (see cfBlockInInput)
   f4 probe = f4{};
+  const int inU = cfUnitsInInput(a, tile, a.Wu);
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     const int g = tid + kCfThreads * j;
@@ -309,7 +336,7 @@ __device__ __forceinline__ void cfStatsLocal(const CfFirArgs& a, const CfWindow<
     bm = fmaxf(bm, __shfl_xor(bm, 2));
     bm = fmaxf(bm, __shfl_xor(bm, 4));
     m = fmaxf(m, um);
-    if (bm > 0.0f) bmin = fminf(bmin, bm);
+    if (bm > 0.0f || cfBlockInInput(g, inU)) bmin = fminf(bmin, bm);
   }
   const float pr = (probe.x + probe.y) + (probe.z + probe.w);
   if (pr != pr) m = INFINITY;  // non-finite sample: direct path
@@ -341,9 +368,9 @@ __device__ __forceinline__ bool cfStatsFinish(const float (*red)[kCfWaves], int*
 
 // Both halves with their own barriers (prologue and the single-set kernel).
 template <int G>
-__device__ __forceinline__ bool cfTileStats(const CfFirArgs& a, const CfWindow<G>& w, int tid, float (*red)[kCfWaves],
-                                            int* sxOut) {
-  cfStatsLocal<G>(a, w, tid, red);
+__device__ __forceinline__ bool cfTileStats(const CfFirArgs& a, const CfWindow<G>& w, int tile, int tid,
+                                            float (*red)[kCfWaves], int* sxOut) {
+  cfStatsLocal<G>(a, w, tile, tid, red);
   __syncthreads();
   const bool d = cfStatsFinish(red, sxOut);
   __syncthreads();  // red[] is rewritten by the next tile's statistics
@@ -437,7 +464,7 @@ __device__ __forceinline__ void cfF16Tile(const CfFirArgs& a, int8_t* smem, floa
     for (int k = 0; k < 16; ++k) part[(wave * 16 + k) * kWave + lane] = acc[k];
   }
   // tile i + 2's statistics (its loads had the MFMA phase to land); red2 alternates by tile
-  if (i + 2 < n) cfStatsLocal<G>(a, wNext, tid, red2[i & 1]);
+  if (i + 2 < n) cfStatsLocal<G>(a, wNext, tile + 2, tid, red2[i & 1]);
   __syncthreads();  // partials and statistics published; `cur` read and `nxt` written by all waves
   CfF16State nn{0, true};
   if (i + 2 < n) nn.direct = cfStatsFinish(red2[i & 1], &nn.sx);
@@ -529,14 +556,14 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfF16MfmaKernel(CfFirArgs a)
 
   // ---- prologue: tile t0 into plane set 0; tile t0 + 1's window and statistics ---------------
   CfF16State st{0, true};
-  st.direct = cfTileStats<G>(a, winB, tid, red, &st.sx);
+  st.direct = cfTileStats<G>(a, winB, t0, tid, red, &st.sx);
   if (!st.direct) splitWindowF16<G>(a, winB, smem, tid, ldexpf(1.0f, st.sx));
   if (n > 1) loadWindow<G>(a, t0 + 1, tid, winA);
   __syncthreads();
 
   if constexpr (DB) {
     CfF16State nx{0, true};
-    if (n > 1) nx.direct = cfTileStats<G>(a, winA, tid, red, &nx.sx);
+    if (n > 1) nx.direct = cfTileStats<G>(a, winA, t0 + 1, tid, red, &nx.sx);
     for (int i = 0; i < n; i += 2) {
       cfF16Tile<KS, G, EPI>(a, smem, part, red2, bh, bl, sh, i, n, t0, tid, winA, winB, st, nx);
       if (i + 1 < n)
@@ -591,7 +618,7 @@ __global__ __launch_bounds__(kCfThreads, 1) void firCfF16MfmaKernel(CfFirArgs a)
       if (i + 1 < n) {
         // the next tile's statistics (two barriers, which also fence this tile's partial reads),
         // its planes, then the loads of the one after
-        st.direct = cfTileStats<G>(a, win, tid, red, &st.sx);
+        st.direct = cfTileStats<G>(a, win, tile + 1, tid, red, &st.sx);
         if (!st.direct) splitWindowF16<G>(a, win, smem, tid, ldexpf(1.0f, st.sx));
         if (i + 2 < n) loadWindow<G>(a, tile + 2, tid, win);
         __syncthreads();
@@ -695,9 +722,11 @@ __device__ __forceinline__ void wsSplitGroup(const CfFirArgs& a, int Wl, const C
 
 // Producer-local statistics of a window (as cfStatsLocal over the producer threads).
 template <int G>
-__device__ __forceinline__ void wsStatsLocal(int Wl, const CfWindow<G>& w, int ptid, WsCtl* c, int parity) {
+__device__ __forceinline__ void wsStatsLocal(const CfFirArgs& a, int Wl, int tile, const CfWindow<G>& w, int ptid,
+                                             WsCtl* c, int parity) {
   const int lane = ptid & (kWave - 1);
   const int pw = ptid >> 6;
+  const int inU = cfUnitsInInput(a, tile, Wl);  // units past Wl are not loaded (zeros)
   // on the bit patterns of |x|: a NaN pattern exceeds +inf's, so M > 3e38 (or NaN) sends a tile
   // holding a non-finite sample to the direct path without a separate probe
   uint32_t mu = 0, bminu = 0x7f800000u;
@@ -706,16 +735,15 @@ __device__ __forceinline__ void wsStatsLocal(int Wl, const CfWindow<G>& w, int p
     uint32_t um = 0;  // units past Wl read as zeros: no effect on either statistic
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f4 v = w.v[j][q];
-      const uint32_t a0 = __builtin_bit_cast(uint32_t, v.x) & 0x7fffffffu;
-      const uint32_t a1 = __builtin_bit_cast(uint32_t, v.y) & 0x7fffffffu;
-      const uint32_t a2 = __builtin_bit_cast(uint32_t, v.z) & 0x7fffffffu;
-      const uint32_t a3 = __builtin_bit_cast(uint32_t, v.w) & 0x7fffffffu;
-      um = max(max(um, a0), max(max(a1, a2), a3));
+      // the whole vector cast, then its lanes: this compiler's __builtin_bit_cast of an ext-vector ELEMENT
+      // (v.y, v.z, v.w) reads element 0 - r06 found the statistics had seen only every other sample (a lone
+      // impulse or NaN at an odd sample missed; tests/test_mfma_guard.py)
+      const u4v b = __builtin_bit_cast(u4v, w.v[j][q]) & 0x7fffffffu;
+      um = max(max(um, b.x), max(max(b.y, b.z), b.w));
     }
     const uint32_t bm = dppMax8u(um);  // 64-sample block = 8 consecutive units = 8 consecutive lanes
     mu = max(mu, um);
-    if (bm > 0) bminu = min(bminu, bm);
+    if (bm > 0 || cfBlockInInput(ptid + kWsPThreads * j, inU)) bminu = min(bminu, bm);
   }
   const float m = __builtin_bit_cast(float, waveMaxU(mu));
   const float bmin = __builtin_bit_cast(float, waveMinU(bminu));
@@ -726,12 +754,15 @@ __device__ __forceinline__ void wsStatsLocal(int Wl, const CfWindow<G>& w, int p
 }
 
 __device__ __forceinline__ bool wsStatsFinish(const WsCtl* c, int parity, int* sxOut) {
-  float M = c->stat[parity][0][0], B = c->stat[parity][1][0];
+  // on the bit patterns (the statistics are |x| patterns): fmaxf would drop a NaN wave maximum
+  uint32_t Mu = __builtin_bit_cast(uint32_t, c->stat[parity][0][0]);
+  uint32_t Bu = __builtin_bit_cast(uint32_t, c->stat[parity][1][0]);
 #pragma unroll
   for (int v = 1; v < kWsProducers; ++v) {
-    M = fmaxf(M, c->stat[parity][0][v]);
-    B = fminf(B, c->stat[parity][1][v]);
+    Mu = max(Mu, __builtin_bit_cast(uint32_t, c->stat[parity][0][v]));
+    Bu = min(Bu, __builtin_bit_cast(uint32_t, c->stat[parity][1][v]));
   }
+  const float M = __builtin_bit_cast(float, Mu), B = __builtin_bit_cast(float, Bu);
   *sxOut = 0;
   if (!(M <= 3.0e38f)) return true;
   if (M == 0.0f) return false;
@@ -763,7 +794,7 @@ __device__ __forceinline__ void wsProducerTile(const CfFirArgs& a, int Wl, int8_
   // unconditional (past the last tile: statistics of an empty window, never read), so that every
   // path waits for wNext's loads at the same point and the loop-carried wait counts stay exact
   wsWaitWindow<4 * G>(wNext);
-  wsStatsLocal<G>(Wl, wNext, ptid, c, (i + 1) & 1);
+  wsStatsLocal<G>(a, Wl, tile + 1, wNext, ptid, c, (i + 1) & 1);
   wsSignal(&c->pstat, lane);
 }
 
@@ -1039,7 +1070,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void firCfWsKernel(CfFirArgs a, int 
 #pragma unroll
     for (int j = 0; j < G; ++j) wsLoadGroup<G>(r1, Wl, ptid, j, wB);
     wsWaitWindow<4 * G>(wA);
-    wsStatsLocal<G>(Wl, wA, ptid, c, 0);
+    wsStatsLocal<G>(a, Wl, t0, wA, ptid, c, 0);
     wsSignal(&c->pstat, lane);
     // the back-edge only after the second tile: a path that skipped it would leave wA's loads as
     // the newest on entry and make the compiler's wait counts conservative for both windows

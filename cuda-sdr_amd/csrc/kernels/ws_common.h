@@ -343,7 +343,7 @@ __device__ __forceinline__ void wsI8DrainWindows(I8WsWindow<G>& a, I8WsWindow<G>
 // such taps - at a zero-padded stream start, after an exact-zero gap - misses the 1e-6 sum|h||x| bound.
 // Such a window's samples under every other tap are zero, i.e. the tile window holds a long run of exact
 // complex zeros. A wave flags its part of the window when two consecutive 8-sample units of its 64 are all
-// zero (I = Q = 0; units past Wl excluded): any zero run of >= 31 samples is caught (>= 3 whole units, two
+// zero (I = Q = 0; units past Wl or past the input's end excluded): any zero run of >= 31 samples is caught (>= 3 whole units, two
 // of them in one wave's 64), and the violating runs are ~T long. Flagged tiles are computed in the direct
 // fp32 form by the consumers (wsI8DirectOutput). An adversarial comb - non-zero samples only where a
 // windowed sinc has its zeros - is not a run and stays uncaught. Cost: 3 VALU per unit.
@@ -426,6 +426,9 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
   int8_t* planes = smem + set * 2 * a.planeStride;
   const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
   bool zrun = false;
+  // units wholly inside the input: the last tile's window runs past it (zeros, out of range), not a run
+  const int64_t inU = (a.nIn - (int64_t)tile * kCfTileOut * a.D) >> 3;
+  const int Wz = inU < Wl ? (int)(inU > 0 ? inU : 0) : Wl;
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     const int g = ptid + kWsPThreads * j;
@@ -433,7 +436,7 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
                                __builtin_amdgcn_alignbyte(wCur.q[j].z, wCur.q[j].y, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.q[j].w, wCur.q[j].z, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.e[j], wCur.q[j].w, a.sub)};
-    zrun |= wsI8ZeroRun(words, g < Wl);
+    zrun |= wsI8ZeroRun(words, g < Wz);
     if constexpr (Q8) {
       uint2 iu, qu;
       int8IqToI8Units(words, iu, qu);

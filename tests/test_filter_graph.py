@@ -274,13 +274,16 @@ def test_frequency_shifter_fm_chain(graph, queue, orc):
     assert np.max(err) <= 5e-2, (int(np.argmax(err)), float(np.max(err)))
 
 
-def _am_chain_graph(graph, queue, taps, D):
-    """int8 IQ -> Int8ToFloat -> Fir -> QuadAmDemod -> HipMemcpy (device -> host), all on one queue;
-    the D2H filter is the graph tail the driver pulls through."""
+def _am_chain_graph(graph, queue, taps, D, qname="qg"):
+    """int8 IQ -> Int8ToFloat -> Fir -> QuadAmDemod -> HipMemcpy (device -> host), all on one queue
+    (`qname` names `queue`: the D2H filter is created from JSON, which names its queue - r06: the
+    fixed-frame test passed "qf" but got a D2H on "qg", another stream, and its reference stream read
+    one step's last AM sample before the AM kernel had written it, once in ~40 runs); the D2H filter
+    is the graph tail the driver pulls through."""
     conv = graph.Node.int8_to_float(queue)
     fir = graph.Node.fir(queue, taps, D, graph.SAMPLE_FLOAT_COMPLEX)
     am = graph.Node.quad_am_demod(queue)
-    d2h = graph.Node.from_json("HipMemcpy", '{"commandQueue": "qg", "from": "device", "to": "host"}', queue)
+    d2h = graph.Node.from_json("HipMemcpy", '{"commandQueue": "%s", "from": "device", "to": "host"}' % qname, queue)
     drv = graph.SteppingDriver()
     drv.connect(conv, 0, fir, 0)
     drv.connect(fir, 0, am, 0)
@@ -335,7 +338,7 @@ def test_graph_stepping_falls_back_for_a_tone_source(graph, orc):
     for mode in ("eager", "graphed"):
         src = graph.Node.cosine(queue, graph.SAMPLE_FLOAT_COMPLEX, 48000.0, 1000.0)
         am = graph.Node.quad_am_demod(queue)
-        d2h = graph.Node.from_json("HipMemcpy", '{"commandQueue": "qg", "from": "device", "to": "host"}', queue)
+        d2h = graph.Node.from_json("HipMemcpy", '{"commandQueue": "%s", "from": "device", "to": "host"}' % qname, queue)
         drv = graph.SteppingDriver()
         drv.connect(src, 0, am, 0)
         drv.connect(am, 0, d2h, 0)
@@ -403,7 +406,7 @@ def test_host_egress_sink_fixed_frame_reader(graph, orc):
     taps = orc.lowpass_taps(T, 0.2)
     rng = np.random.default_rng(34)
     iq = rng.integers(-128, 128, size=2 * chunk * steps).astype(np.int8)
-    conv, tail, drv = _am_chain_graph(graph, queue, taps, D)
+    conv, tail, drv = _am_chain_graph(graph, queue, taps, D, "qf")
     ref = []
     for s in range(steps):
         conv.push(iq[2 * chunk * s: 2 * chunk * (s + 1)])

@@ -137,6 +137,34 @@ def test_int8_mfma_zero_padded_windows(ops, orc, T, D, cut, window, kernel):
     _check(am, np.abs(y64), bound, ("int8-am", kernel, T, D))
 
 
+def _burst_onset_iq(n, quiet, seed):
+    """int8 IQ: +-quiet LSB of noise for the first half, then full-scale noise (a burst onset)."""
+    rng = np.random.default_rng(seed)
+    q = np.where(np.arange(2 * n) < n, rng.integers(-quiet, quiet + 1, 2 * n), rng.integers(-128, 128, 2 * n))
+    return q.astype(np.int8)
+
+
+@pytest.mark.parametrize("T,D,cut,window,kernel", [(1023, 10, 0.04, "blackman", "i8-dec-mfma"),
+                                                   (255, 5, 0.08, "blackman", "i8-dec-mfma"),
+                                                   (127, 1, 0.1, "hamming", "i8-mfma")])
+def test_int8_mfma_burst_onset(ops, orc, T, D, cut, window, kernel):
+    """VERDICT r05 item 3's int8 x int8 form fails here (tools/exp/q8_tap_error.py --burst: 1.7-2.4x the
+    bound): the windows with a full-scale burst under the tail taps and +-1 LSB under the large ones. The
+    product's f16 x 2 tap limbs keep each tap to 2^-22 of itself: per element within the bound."""
+    iq = _burst_onset_iq(120_000, 1, T)
+    n_in = len(iq) // 2
+    n_out = (n_in - T) // D + 1
+    taps = orc.lowpass_taps(T, cut, window)
+    x_d, taps_d = _dev(iq), _dev(taps)
+    assert ops.fir_kernel_class(x_d, taps_d, D, int8_iq=True) == kernel
+    y = _host(ops.fir(taps_d, x_d, D, n_out, int8_iq=True))
+    am = _host(ops.fir(taps_d, x_d, D, n_out, int8_iq=True, am=True))
+    xc = orc.int8_to_float(iq).view(np.complex64)
+    y64, bound = orc.fir_f64(taps, xc, D, n_out)
+    _check(y, y64, bound, ("int8-burst", kernel, T, D))
+    _check(am, np.abs(y64), bound, ("int8-burst-am", kernel, T, D))
+
+
 def test_fused_chain_zero_padded_windows(ops, orc):
     """The fused C5 chain (RF FIR -> AM -> audio FIR in one launch) over the zero-gapped stream: the AM
     samples against float64 per element, the audio within the carried bound."""
