@@ -106,9 +106,11 @@ __device__ __forceinline__ const f4* w4Part(const float* part, int b, int v, int
 // this lane (AUD: held for the ring, and stored when the caller asked for the AM samples), or the outputs
 // stored right away. Accumulator register i = wave + 4 h holds row (i & 3) + 8 (i >> 2) + 4 half of the
 // 32 x 32 tile.
+// skip: the zero-window guard's tile (its outputs are the producers', w4DirectTile / w4PatchRing): no
+// global store (AUD: the AM samples still go to the ring, where the producers overwrite them).
 template <int EPI, bool AUD>
 __device__ __forceinline__ void w4Outputs(const I8DecArgs& a, float outScale, int tile, int j, int tid, f4 y, bool lead,
-                                          float (&am)[2]) {
+                                          float (&am)[2], bool skip) {
   const int lane = tid & (kWave - 1);
   const int wave = tid >> 6;
   const int half = lane >> 5, col = lane & 31;
@@ -121,8 +123,8 @@ __device__ __forceinline__ void w4Outputs(const I8DecArgs& a, float outScale, in
       const float v = __builtin_amdgcn_sqrtf(fmaf(yi[h], yi[h], yq[h] * yq[h])) * outScale;
       am[h] = k < a.nOut ? v : 0.0f;
       // the lead tile belongs to the previous block (computed here only for the audio windows)
-      if (a.out != nullptr && k < a.nOut && !(lead && j == 0)) reinterpret_cast<float*>(a.out)[k] = v;
-    } else if (k < a.nOut) {
+      if (a.out != nullptr && k < a.nOut && !(lead && j == 0) && !skip) reinterpret_cast<float*>(a.out)[k] = v;
+    } else if (k < a.nOut && !skip) {
       if (EPI == kEpiAm)
         reinterpret_cast<float*>(a.out)[k] = __builtin_amdgcn_sqrtf(fmaf(yi[h], yi[h], yq[h] * yq[h])) * outScale;
       else
@@ -148,18 +150,67 @@ __device__ __forceinline__ void w4RingWrite(float* ring, int j, int tid, const f
   }
 }
 
-// The zero-window guard's tiles (ws_common.h wsI8ZeroRun): this lane's two outputs of tile `tile` in the
-// direct fp32 form, as the sums w4Outputs takes {yi0, yi1, yq0, yq1}.
-__device__ __forceinline__ f4 w4DirectY(const I8DecArgs& a, int tile, int tid, int sh) {
-  const int lane = tid & (kWave - 1);
-  const int wave = tid >> 6;
-  float yi[2] = {0.0f, 0.0f}, yq[2] = {0.0f, 0.0f};
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int64_t k = (int64_t)tile * kCfTileOut + 32 * (wave + 8 * h + 4 * (lane >> 5)) + (lane & 31);
-    if (k < a.nOut) wsI8DirectOutput(a.iq4 + a.sub, a.taps, a.T, a.D, k, sh, yi[h], yq[h]);
+// The zero-window guard (ws_common.h wsI8ZeroRun) in this kernel: a flagged tile's outputs come from the
+// PRODUCER waves in the direct form (double sums), the consumers skip their stores of it. (r06: the direct
+// form inside the consumer loop cost registers the 168 VGPRs of tap fragments leave no room for - spills
+// in the K loop, C5 0.160 -> 0.202 ms per step.) Plain launches: each producer wave that flags a tile
+// writes all 512 outputs right after handing its planes over (several flagging waves write the same
+// values). Fused chain: the AM samples must be right in the ring before the audio FIR reads them, so
+// the tile's flag goes to a bit mask (zhist, by block-local tile mod 64) and at the audio stage of that
+// tile the four producer waves overwrite its ring slot (and store the AM samples) - after the consumers
+// wrote it, before any window reads it. (The wait in w4PatchRing is then already satisfied.)
+__device__ __forceinline__ float w4DirectValue(const I8DecArgs& a, int64_t k, int epi, float& im) {
+  double si, sq;
+  wsI8DirectSums(a.iq4 + a.sub, a.taps, a.T, a.D, k, si, sq);
+  si *= 1.0 / 127.0;
+  sq *= 1.0 / 127.0;
+  im = (float)sq;
+  // the envelope in double: the guard's outputs can be far below 1 (squares below the fp32 normals)
+  return epi == kEpiAm ? (float)__builtin_sqrt(fma(si, si, sq * sq)) : (float)si;
+}
+
+template <int EPI>
+__device__ __forceinline__ void w4DirectTile(const I8DecArgs& a, int tile, int lane) {
+#pragma unroll 1
+  for (int r = 0; r < kCfTileOut / kWave; ++r) {
+    const int64_t k = (int64_t)tile * kCfTileOut + kWave * r + lane;
+    if (k >= a.nOut) break;
+    float im;
+    const float v = w4DirectValue(a, k, EPI, im);
+    if (EPI == kEpiAm) reinterpret_cast<float*>(a.out)[k] = v;
+    else reinterpret_cast<f2*>(a.out)[k] = f2{v, im};
   }
-  return f4{yi[0], yi[1], yq[0], yq[1]};
+}
+
+// zhist: two words of WsCtl's zflag area the 4-way kernel's two plane sets leave free
+static_assert(kW4Sets <= 2, "zhist / zsync use zflag[2] and zflag[3]");
+__device__ __forceinline__ int* w4Zhist(WsCtl* c) { return &c->zflag[2][0]; }
+__device__ __forceinline__ int* w4Zsync(WsCtl* c) { return &c->zflag[3][0]; }
+
+// Fused chain, producer wave pw, before the audio outputs of block-local tile t: when t was flagged, its
+// AM samples in the direct form into the ring (the 4 waves 128 each), stored when the caller asked for
+// them (not the lead tile's), then all 4 waves meet (zsync, nz flagged tiles so far) before a window
+// reads the slot.
+__device__ __forceinline__ void w4PatchRing(const I8DecArgs& a, float* ring, WsCtl* c, int t0, int t,
+                                                      bool lead, int ptid, int nz) {
+  const int lane = ptid & (kWave - 1);
+  const int pw = ptid >> 6;
+  const bool aborted = wsWaitAb(c, &c->amSlot[t & (kAmRing - 1)], kW4Consumers * (t / kAmRing + 1));
+  if (!aborted) {
+#pragma unroll 1
+    for (int r = 0; r < 2; ++r) {
+      const int idx = 128 * pw + kWave * r + lane;
+      const int64_t k = (int64_t)(t0 + t) * kCfTileOut + idx;
+      float im;
+      const float v = k < a.nOut ? w4DirectValue(a, k, kEpiAm, im) : 0.0f;
+      const int pos = (t & (kAmRing - 1)) * kCfTileOut + idx;
+      ring[pos] = v;
+      if (pos < kAmRingMirror) ring[kAmRing * kCfTileOut + pos] = v;
+      if (a.out != nullptr && k < a.nOut && !(lead && t == 0)) reinterpret_cast<float*>(a.out)[k] = v;
+    }
+  }
+  wsSignal(w4Zsync(c), lane);
+  wsWait(c, w4Zsync(c), kWsProducers * nz);
 }
 
 __device__ __forceinline__ void w4AmFreeWait(WsCtl* c, int j) {  // ring slot of tile j reusable
@@ -286,7 +337,7 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
     if (wave == 0) { W4TR(0, i, 0) }
 #endif
     zPrev = zCur;
-    zCur = wsI8Zflag(c, set);  // read before this tile's planesFree lets the producers rewrite it
+    if (GSDR_WS_ZGUARD & 2) zCur = wsI8Zflag(c, set);  // read before this tile's planesFree lets the producers rewrite it
     const int8_t* pI = smem + set * 2 * a.planeStride + comp * a.planeStride;
 #if GSDR_W4_Q8
     v16i acc0 = v16i{}, acc1 = v16i{}, acc2 = v16i{};
@@ -363,8 +414,7 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
       if (!(GSDR_WS_ABL & 2)) pb[(wave * 4 + r) * kWave + lane] = f4{acc[r], acc[r + 4], acc[r + 8], acc[r + 12]};
       else asm volatile("" ::"v"(acc[r]), "v"(acc[r + 4]), "v"(acc[r + 8]), "v"(acc[r + 12]));
 #if GSDR_W4_LATESIG  // the previous tile's outputs while the partial writes land
-    if (red && zPrev) y = w4DirectY(a, t0 + i - 1, tid, sh);
-    if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am);
+    if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am, zPrev);
     W4ST(6)
     if (GSDR_W4_NOFENCE) {
       asm volatile("" ::: "memory");
@@ -376,8 +426,7 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
 #else
     wsSignal(&c->partsFull[b], lane);
     W4ST(5)
-    if (red && zPrev) y = w4DirectY(a, t0 + i - 1, tid, sh);
-    if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am);
+    if (red) w4Outputs<EPI, AUD>(a, outScale, t0 + i - 1, i - 1, tid, y, lead, am, zPrev);
     W4ST(6)
 #endif
 #ifdef GSDR_W4_STAMPS
@@ -398,8 +447,7 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
 #pragma unroll
     for (int v = 0; v < kW4Consumers; ++v) y += *w4Part(part, rb, v, wave, lane);
     wsSignal(&c->partsFree[rb], lane);
-    if (zCur) y = w4DirectY(a, t0 + j, tid, sh);
-    w4Outputs<EPI, AUD>(a, outScale, t0 + j, j, tid, y, lead, am);
+    w4Outputs<EPI, AUD>(a, outScale, t0 + j, j, tid, y, lead, am, zCur);
     if constexpr (AUD) {
       w4AmFreeWait(c, j);
       w4RingWrite(ring, j, tid, am);
@@ -514,21 +562,51 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
 #else
     unsigned long long* stp = nullptr;
 #endif
+    int nz = 0;  // AUD: flagged tiles patched so far (the zsync target)
+    // AUD: the audio outputs of block-local tile t, after patching its ring slot when it was flagged
+    // (the bit is read once the consumers have put tile t in the ring - its producers set it before the
+    // planes went over; the slot count and the mask in one LDS round trip, the count almost always reached)
+    auto audio = [&](int t) {
+      if (t < n) {
+        int* slot = &c->amSlot[t & (kAmRing - 1)];
+        const int target = kW4Consumers * (t / kAmRing + 1);
+        const int v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        int zh = __hip_atomic_load(&w4Zhist(c)[(t >> 5) & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (waveUniform(v) < target) {
+          wsWait(c, slot, target);
+          zh = __hip_atomic_load(&w4Zhist(c)[(t >> 5) & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (waveUniform(zh) & (1 << (t & 31))) w4PatchRing(a8, ring, c, t0, t, lead, ptid, ++nz);
+      }
+      wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, t, ptid, ht, ab, stp);
+    };
+    // after tile i's planes: a flagged tile's direct outputs (plain) or its bit in zhist (AUD; and the bit
+    // of tile i - 32 cleared: its audio is long done - production leads the audio stage by fewer than
+    // kAmRing + kW4Sets + kAudioLag tiles)
+    auto guard = [&](bool zrun, int i) {
+      if constexpr (AUD) {  // (the bit itself: wsI8ProducerTile, before the planes go over)
+        if (ptid == 0)
+          __hip_atomic_fetch_and(&w4Zhist(c)[((i >> 5) & 1) ^ 1], ~(1 << (i & 31)), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        if (zrun) w4DirectTile<EPI>(a8, t0 + i, lane);
+      }
+    };
+    static_assert(kAmRing + kW4Sets + kAudioLag + 2 < 32, "zhist: a bit is cleared 32 tiles after it was set");
     for (int i = 0;; i += 2) {
-      wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
-        if (AUD && i >= kAudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i - kAudioLag, ptid, ht, ab, stp);
-      }, stp);
+      guard(wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
+        if (AUD && i >= kAudioLag) audio(i - kAudioLag);
+      }, stp, AUD ? w4Zhist(c) : nullptr), i);
       if (i + 1 >= n) break;
-      wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
-        if (AUD && i + 1 >= kAudioLag) wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, i + 1 - kAudioLag, ptid, ht, ab, stp);
-      }, stp);
+      guard(wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
+        if (AUD && i + 1 >= kAudioLag) audio(i + 1 - kAudioLag);
+      }, stp, AUD ? w4Zhist(c) : nullptr), i + 1);
       if (i + 2 >= n) break;
     }
     (void)stp;
     wsI8DrainWindows<G>(wA, wB);  // before the registers can go to the tail's code
     if constexpr (AUD)
-      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t)
-        wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, t, ptid, ht, ab);
+      for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) audio(t);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the wave
 #ifdef GSDR_W4_STAMPS
     if ((int)blockIdx.x == kW4TraceBlock && wave == kW4Consumers && lane == 0)

@@ -347,10 +347,25 @@ __device__ __forceinline__ void wsI8DrainWindows(I8WsWindow<G>& a, I8WsWindow<G>
 // of them in one wave's 64), and the violating runs are ~T long. Flagged tiles are computed in the direct
 // fp32 form by the consumers (wsI8DirectOutput). An adversarial comb - non-zero samples only where a
 // windowed sinc has its zeros - is not a run and stays uncaught. Cost: 3 VALU per unit.
-__device__ __forceinline__ bool wsI8ZeroRun(const uint32_t (&words)[4], bool valid) {
-  const uint32_t o = words[0] | words[1] | words[2] | words[3];
-  const uint64_t zm = __ballot(valid && o == 0u);
-  return (zm & (zm >> 1)) != 0;
+#ifndef GSDR_WS_ZALT  // A/B builds only (r06 guard cost): 1 = validity by Wl alone, 2 = no zhist bit,
+                      // 4 = the zero bits computed, the run test not
+#define GSDR_WS_ZALT 0
+#endif
+#ifndef GSDR_WS_ZGUARD  // A/B builds only: bit 0 the producers' zero runs, bit 1 the 4-way consumers' flag reads
+#define GSDR_WS_ZGUARD 3
+#endif
+// Per unit: bit j of the thread's mask when unit g = ptid + kWsPThreads j is all zero (and valid); per tile,
+// once: a pair of adjacent units (neighbouring lanes, one DPP wave shift) in any lane. (r06: a ballot per
+// unit inside the conversion loop cost the C5 launch 35 us of its 147 - the scalar mask chain serialised the
+// loop; this form is ~3 VALU per unit and 4 instructions per tile.)
+__device__ __forceinline__ uint32_t wsI8ZeroBit(const uint32_t (&words)[4], bool valid, int j) {
+  if (!(GSDR_WS_ZGUARD & 1)) return 0u;
+  return (valid && (words[0] | words[1] | words[2] | words[3]) == 0u) ? (1u << j) : 0u;
+}
+__device__ __forceinline__ bool wsI8ZeroRun(uint32_t zb) {
+  if (!(GSDR_WS_ZGUARD & 1)) return false;
+  const uint32_t nb = (uint32_t)__builtin_amdgcn_mov_dpp((int)zb, 0x130, 0xf, 0xf, true);  // wave_shl:1
+  return __ballot((zb & nb) != 0u) != 0;
 }
 
 // zero-window flags of plane set `set` (the producer waves' zflag words, read after planesFull)
@@ -358,26 +373,30 @@ __device__ __forceinline__ bool wsI8Zflag(const WsCtl* c, int set) {
   return waveUniform(c->zflag[set][0] | c->zflag[set][1] | c->zflag[set][2] | c->zflag[set][3]) != 0;
 }
 
-// Direct fp32 form of int8 IQ output k (the guard's tiles): {sum_j h_j I'_kD+j, sum_j h_j Q'_kD+j} with
-// x' = max(x, -127), 64-tap blocked partial sums (the VALU kernels' order class), in the MFMA path's
-// scaled units (x 2^sh) so the caller's epilogue (x 2^-sh / 127) applies unchanged.
+// Direct form of int8 IQ output k (the guard's tiles): sum_j h_j I'_kD+j and sum_j h_j Q'_kD+j with
+// x' = max(x, -127), accumulated in double (rare tiles; a sequential fp32 sum of ~1 000 products can
+// reach 1e-6 of sum|h||x|, tests/test_mfma_guard.py). Not unrolled: little code, few registers.
+__device__ __forceinline__ void wsI8DirectSums(const int8_t* iq, const float* taps, int T, int D, int64_t k, double& si,
+                                               double& sq) {
+  const int8_t* p = iq + 2 * k * D;
+  si = 0.0;
+  sq = 0.0;
+#pragma unroll 1
+  for (int j = 0; j < T; ++j) {
+    const double h = taps[j];
+    si = fma(h, (double)max((int)p[2 * j], -127), si);
+    sq = fma(h, (double)max((int)p[2 * j + 1], -127), sq);
+  }
+}
+
+// The same in the MFMA path's scaled units (x 2^sh), for the 8-way kernel's consumers (their epilogue,
+// x 2^-sh / 127, applies unchanged).
 __device__ __forceinline__ void wsI8DirectOutput(const int8_t* iq, const float* taps, int T, int D, int64_t k, int sh,
                                                  float& yi, float& yq) {
-  const int8_t* p = iq + 2 * k * D;
-  float si = 0.0f, sq = 0.0f;
-  for (int j0 = 0; j0 < T; j0 += 64) {
-    const int j1 = T < j0 + 64 ? T : j0 + 64;
-    float pi = 0.0f, pq = 0.0f;
-    for (int j = j0; j < j1; ++j) {
-      const float h = taps[j];
-      pi = fmaf(h, (float)max((int)p[2 * j], -127), pi);
-      pq = fmaf(h, (float)max((int)p[2 * j + 1], -127), pq);
-    }
-    si += pi;
-    sq += pq;
-  }
-  yi = ldexpf(si, sh);
-  yq = ldexpf(sq, sh);
+  double si, sq;
+  wsI8DirectSums(iq, taps, T, D, k, si, sq);
+  yi = (float)ldexp(si, sh);
+  yq = (float)ldexp(sq, sh);
 }
 
 // Producer, tile i: wCur holds tile i's window (complete after the wait), wNext tile i + 1's.
@@ -393,10 +412,13 @@ struct NoPre {
 // NS plane sets: tile i goes to set i % NS once the consumers are done with tile i - NS. Q8: int8 planes
 // (the 4-way kernel's int8 x int8 MFMA form): the 8 samples of a group are one 8-byte half of a 16-byte
 // plane slot, slot g / 2 (padded like the f16 units), half g % 2.
+// Returns whether this wave's part of the window holds a zero run (the zero-window guard, wsI8ZeroRun).
 template <int G, int NC = kCfWaves, int NS = 2, bool Q8 = false, typename Pre = NoPre>
-__device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
+// zhist (the 4-way kernel's fused chain): a flagged tile's bit (block-local index mod 64), set before the
+// planes are handed over - so before the consumers write the tile's AM samples to the ring.
+__device__ __forceinline__ bool wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
                                                  int i, int ptid, I8WsWindow<G>& wCur, const Pre& pre = Pre{},
-                                                 unsigned long long* st = nullptr) {
+                                                 unsigned long long* st = nullptr, int* zhist = nullptr) {
   const int lane = ptid & (kWave - 1);
   const int set = i % NS;
 #if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
@@ -425,7 +447,7 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 #endif
   int8_t* planes = smem + set * 2 * a.planeStride;
   const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
-  bool zrun = false;
+  uint32_t zb = 0;
   // units wholly inside the input: the last tile's window runs past it (zeros, out of range), not a run
   const int64_t inU = (a.nIn - (int64_t)tile * kCfTileOut * a.D) >> 3;
   const int Wz = inU < Wl ? (int)(inU > 0 ? inU : 0) : Wl;
@@ -436,7 +458,7 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
                                __builtin_amdgcn_alignbyte(wCur.q[j].z, wCur.q[j].y, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.q[j].w, wCur.q[j].z, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.e[j], wCur.q[j].w, a.sub)};
-    zrun |= wsI8ZeroRun(words, g < Wz);
+    zb |= wsI8ZeroBit(words, (GSDR_WS_ZALT & 1) ? g < Wl : g < Wz, j);
     if constexpr (Q8) {
       uint2 iu, qu;
       int8IqToI8Units(words, iu, qu);
@@ -468,7 +490,11 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
     wsI8LoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
   }
   if (ptid == 0) c->mode[set] = 0;
+  if (GSDR_WS_ZALT & 4) asm volatile("" ::"v"(zb));
+  const bool zrun = (GSDR_WS_ZALT & 4) ? false : wsI8ZeroRun(zb);
   if (lane == 0) c->zflag[set][ptid >> 6] = zrun ? 1 : 0;  // published by the planesFull release
+  if (!(GSDR_WS_ZALT & 2) && zhist != nullptr && zrun && lane == 0)
+    __hip_atomic_fetch_or(&zhist[(i >> 5) & 1], 1 << (i & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   wsSignal(&c->planesFull[set], lane);
 #if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
   if (st) st[3] += __builtin_amdgcn_s_memtime() - t0s;
@@ -476,6 +502,7 @@ __device__ __forceinline__ void wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 #ifdef W4TR
   if (ptid < kWave) { W4TR(1, i, 3) }
 #endif
+  return zrun;
 }
 
 

@@ -338,7 +338,7 @@ def test_graph_stepping_falls_back_for_a_tone_source(graph, orc):
     for mode in ("eager", "graphed"):
         src = graph.Node.cosine(queue, graph.SAMPLE_FLOAT_COMPLEX, 48000.0, 1000.0)
         am = graph.Node.quad_am_demod(queue)
-        d2h = graph.Node.from_json("HipMemcpy", '{"commandQueue": "%s", "from": "device", "to": "host"}' % qname, queue)
+        d2h = graph.Node.from_json("HipMemcpy", '{"commandQueue": "qg", "from": "device", "to": "host"}', queue)
         drv = graph.SteppingDriver()
         drv.connect(src, 0, am, 0)
         drv.connect(am, 0, d2h, 0)

@@ -123,3 +123,35 @@ def test_no_memory_instruction_under_a_landing_load(chk, ws_kernels):
     assert len(ws_kernels) >= 200
     bad = {n: chk.memory_hazards(h)[:3] for n, h in ws_kernels.items() if chk.memory_hazards(h)}
     assert not bad, bad
+
+
+def test_product_kernels_do_not_spill(chk):
+    """No register spill in the kernels the bench lines and the default paths run (r06: the zero-window
+    guard's direct form inside the 4-way kernel's consumer loop pushed its tap fragments to scratch - a
+    reload every tile, C5 0.160 -> 0.202 ms per step; the guard's work moved to the producer waves). C5's
+    fused and plain 4-way kernels (KS = 21, G = 3), every 8-way int8 kernel, every cf32 wave-specialised
+    kernel, C2's int8 kernel. (The 4-way K = 1408 instantiations, KS = 22, spill and are not asserted.)"""
+    objs = _objects()
+    objs["fir_i8_mfma.o"] = os.path.join(BUILD, "fir_i8_mfma.o")
+    meta = {}
+    for path in objs.values():
+        meta.update(chk.kernel_metadata(path))
+    want = [n for n in meta if ("firI8Ws4KernelILi21ELi3E" in n or "firI8WsKernel" in n or "firCfWsKernel" in n
+                                or "firI8MfmaKernelILi5ELi2E" in n)]
+    assert len(want) >= 100, len(want)
+    spilled = {n: meta[n] for n in want if meta[n]["vgpr_spill_count"] or meta[n]["sgpr_spill_count"]}
+    assert not spilled, spilled
+
+
+def test_no_bit_cast_of_a_vector_element():
+    """This compiler reads element 0 for `__builtin_bit_cast(T, v.y)` when `v` is an ext vector (r06: the cf32
+    WS kernels' statistics saw every other sample). No kernel source may use the pattern."""
+    import re
+    pat = re.compile(r"__builtin_bit_cast\(\s*[\w:]+\s*,\s*[^(),]*\.[xyzw]\s*\)")
+    src = os.path.join(REPO, "cuda-sdr_amd", "csrc", "kernels")
+    hits = []
+    for path in sorted(glob.glob(os.path.join(src, "*.hip")) + glob.glob(os.path.join(src, "*.h"))):
+        for n, line in enumerate(open(path), 1):
+            if pat.search(line):
+                hits.append(f"{os.path.basename(path)}:{n}: {line.strip()}")
+    assert not hits, hits

@@ -57,6 +57,34 @@ def disassemble(path: str) -> str:
         return out.stdout
 
 
+def kernel_metadata(path: str) -> dict:
+    """{kernel symbol: {vgpr_count, agpr_count, vgpr_spill_count, sgpr_spill_count, private_segment_fixed_size}}
+    from the code object's notes (llvm-readelf --notes). r06: a register spill inside a hot loop (the C5
+    kernel's K loop reloaded a tap fragment from scratch every tile) costs more than any tuning gains."""
+    with tempfile.TemporaryDirectory() as td:
+        co = path
+        fb = os.path.join(td, "fb.bin")
+        r = subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", path, fb], capture_output=True)
+        if r.returncode == 0 and os.path.getsize(fb) > 0:
+            co = os.path.join(td, "k.co")
+            subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={fb}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], capture_output=True, text=True,
+                               check=True).stdout
+    out = {}
+    keys = ("vgpr_count", "agpr_count", "vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size")
+    for blk in notes.split(".name:")[1:]:
+        name = blk.split("\n")[0].strip()
+        if name.endswith(".kd"):
+            continue
+        meta = {}
+        for k in keys:
+            m = re.search(r"\." + k + r":\s+(\d+)", blk)
+            meta[k] = int(m.group(1)) if m else 0
+        out[name] = meta
+    return out
+
+
 def regs(text: str) -> set:
     s = set()
     for m in _VR.finditer(text):
