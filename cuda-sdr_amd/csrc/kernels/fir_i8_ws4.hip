@@ -53,6 +53,8 @@ constexpr int kW4Consumers = 4;                                    // one per SI
 constexpr int kW4Sets = GSDR_W4_SETS;  // plane sets: the producers fill tile i while tiles i - kW4Sets + 1 .. i - 1 wait
 constexpr int kW4Threads = (kW4Consumers + kWsProducers) * kWave;  // 512
 constexpr int kW4PartialBytes = kW4Consumers * 16 * kWave * 4;     // 16 KB per partial buffer
+constexpr int kW4RingBytes = 4 * (kAmRing * kCfTileOut + kAmRingMirror);  // the fused chain's AM ring
+constexpr int kW4ZlaneBytes = 4 * 2 * kWsPThreads;                 // the zero-window guard's pair minima, 2 sets
 #ifndef GSDR_W4_Q8
 #define GSDR_W4_Q8 0
 #endif
@@ -250,7 +252,7 @@ __device__ __forceinline__ bool w4Ready(WsCtl* c, const int* p0, int g0, const i
 // round trips); then the partials of this tile, and the previous tile's outputs formed in registers.
 template <int KS, int EPI, bool AUD>
 __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* smem, float* part, WsCtl* c, int sh,
-                                            int t0, int n, int tid, float* ring, bool lead) {
+                                            int t0, int n, int tid, float* ring, bool lead, const uint32_t* zlane) {
   constexpr int PF = GSDR_W4_PF < KS ? GSDR_W4_PF : KS;
   const int lane = tid & (kWave - 1);
   const int wave = waveUniform(tid >> 6);
@@ -337,7 +339,13 @@ __device__ __forceinline__ void w4Consumers(const I8DecArgs& a, const int8_t* sm
     if (wave == 0) { W4TR(0, i, 0) }
 #endif
     zPrev = zCur;
-    if (GSDR_WS_ZGUARD & 2) zCur = wsI8Zflag(c, set);  // read before this tile's planesFree lets the producers rewrite it
+    if (GSDR_WS_ZGUARD & 2) {  // read before this tile's planesFree lets the producers rewrite it
+      // the producer threads' pair minima (ws_common.h wsI8ZeroPair), four waves' per ds_read_b128
+      const u4v zl = *reinterpret_cast<const u4v*>(zlane + set * kWsPThreads + 4 * lane);
+      zCur = __ballot(min(min(zl.x, zl.y), min(zl.z, zl.w)) == 0u) != 0;
+      if (zCur && wave == 0 && lane == 0)  // for the producers (direct outputs / ring patch), before planesFree
+        __hip_atomic_fetch_or(&w4Zhist(c)[(i >> 5) & 1], 1 << (i & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     const int8_t* pI = smem + set * 2 * a.planeStride + comp * a.planeStride;
 #if GSDR_W4_Q8
     v16i acc0 = v16i{}, acc1 = v16i{}, acc2 = v16i{};
@@ -470,6 +478,8 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   float* part = reinterpret_cast<float*>(smem + 2 * kW4Sets * a8.planeStride);
   float* ring = AUD ? reinterpret_cast<float*>(smem + 2 * kW4Sets * a8.planeStride + 2 * kW4PartialBytes) : nullptr;
+  uint32_t* zlane = reinterpret_cast<uint32_t*>(smem + 2 * kW4Sets * a8.planeStride + 2 * kW4PartialBytes +
+                                                (AUD ? kW4RingBytes : 0));
   __shared__ WsCtl ctl;
   __shared__ float waveMax[kW4Consumers + kWsProducers];
   WsCtl* c = &ctl;
@@ -580,31 +590,40 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
       }
       wsAudioTile<kW4Consumers>(a8, ring, c, t0, n, lead, t, ptid, ht, ab, stp);
     };
-    // after tile i's planes: a flagged tile's direct outputs (plain) or its bit in zhist (AUD; and the bit
-    // of tile i - 32 cleared: its audio is long done - production leads the audio stage by fewer than
-    // kAmRing + kW4Sets + kAudioLag tiles)
-    auto guard = [&](bool zrun, int i) {
-      if constexpr (AUD) {  // (the bit itself: wsI8ProducerTile, before the planes go over)
-        if (ptid == 0)
-          __hip_atomic_fetch_and(&w4Zhist(c)[((i >> 5) & 1) ^ 1], ~(1 << (i & 31)), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        if (zrun) w4DirectTile<EPI>(a8, t0 + i, lane);
-      }
+    // after tile i's planes: the zhist bit of tile i - 32 cleared (AUD: its audio is long done - production leads
+    // the audio stage by fewer than kAmRing + kW4Sets + kAudioLag tiles); plain: tile i - 2's direct outputs when
+    // the consumers flagged it (they did at its top, before the planesFree this tile waited for)
+    auto zbit = [&](int t) {
+      return (waveUniform(__hip_atomic_load(&w4Zhist(c)[(t >> 5) & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >>
+              (t & 31)) & 1;
+    };
+    auto guard = [&](int i) {
+      if (ptid == 0)
+        __hip_atomic_fetch_and(&w4Zhist(c)[((i >> 5) & 1) ^ 1], ~(1 << (i & 31)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+      if constexpr (!AUD)
+        if (i >= 2 && zbit(i - 2)) w4DirectTile<EPI>(a8, t0 + i - 2, lane);
     };
     static_assert(kAmRing + kW4Sets + kAudioLag + 2 < 32, "zhist: a bit is cleared 32 tiles after it was set");
     for (int i = 0;; i += 2) {
-      guard(wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
+      wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i, i, ptid, wA, [&] {
         if (AUD && i >= kAudioLag) audio(i - kAudioLag);
-      }, stp, AUD ? w4Zhist(c) : nullptr), i);
+      }, stp, zlane);
+      guard(i);
       if (i + 1 >= n) break;
-      guard(wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
+      wsI8ProducerTile<G, kW4Consumers, kW4Sets, kW4Q8>(a8, Wl, smem, c, n, t0 + i + 1, i + 1, ptid, wB, [&] {
         if (AUD && i + 1 >= kAudioLag) audio(i + 1 - kAudioLag);
-      }, stp, AUD ? w4Zhist(c) : nullptr), i + 1);
+      }, stp, zlane);
+      guard(i + 1);
       if (i + 2 >= n) break;
     }
     (void)stp;
     wsI8DrainWindows<G>(wA, wB);  // before the registers can go to the tail's code
+    if constexpr (!AUD)  // the last two tiles, once the consumers are past their tops
+      for (int t = n > 2 ? n - 2 : 0; t < n; ++t) {
+        wsWait(c, &c->planesFree[t % kW4Sets], kW4Consumers * (t / kW4Sets + 1));
+        if (zbit(t)) w4DirectTile<EPI>(a8, t0 + t, lane);
+      }
     if constexpr (AUD)
       for (int t = n > kAudioLag ? n - kAudioLag : 0; t < n; ++t) audio(t);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the wave
@@ -627,7 +646,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void firI8Ws4Kernel(I8DecArgs a8, in
 #endif
     return;
   }
-  w4Consumers<KS, EPI, AUD>(a8, smem, part, c, sh, t0, n, tid, ring, lead);
+  w4Consumers<KS, EPI, AUD>(a8, smem, part, c, sh, t0, n, tid, ring, lead, zlane);
 #if GSDR_WS_WAITS
   wsSpanStore(__builtin_amdgcn_s_memtime() - span0);
 #endif
@@ -740,8 +759,8 @@ hipError_t launchFirI8Ws4(I8DecArgs a, int ksteps, int epi, bool audio, hipStrea
   a.Wu = 60 * a.D + kW4KStep / 2 * a.KS;  // window units (8 samples) per tile: 480 D + 4 kW4KStep KS samples
   const int Wl = std::min(a.Wu, (511 * a.D + a.T + 7) / 8);
   if (Wl > 4 * kWsPThreads) return hipErrorNotSupported;
-  const size_t ringBytes = audio ? sizeof(float) * (kAmRing * kCfTileOut + kAmRingMirror) : 0;
-  const size_t extra = 2 * (size_t)kW4PartialBytes + ringBytes;
+  const size_t ringBytes = audio ? (size_t)kW4RingBytes : 0;
+  const size_t extra = 2 * (size_t)kW4PartialBytes + ringBytes + kW4ZlaneBytes;
   // the layout search costs ~1 ms of host time: cached per (D, KS, audio)
   static std::mutex mu;
   static std::vector<std::pair<uint64_t, CfLayout>> cache;

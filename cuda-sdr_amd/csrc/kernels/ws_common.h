@@ -172,6 +172,20 @@ __device__ __forceinline__ void wsRaiseAbort(WsCtl* c) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The hand-off budget in s_memrealtime ticks (100 MHz), 32 bits: the elapsed time is compared modulo 2^32
+// (42.9 s), so a budget above that saturates. 32-bit scalar compares only - a 64-bit ordered compare is a VALU
+// v_cmp on gfx9, and its mask reaches the scalar branch only after the VALU queue behind the SIMD's MFMAs
+// drains (r06: the C5 launch's producer waves paid that per tile; see wsClampI64).
+__device__ __forceinline__ uint32_t wsBudgetTicks(const WsCtl* c) {
+  const uint32_t us = (uint32_t)waveUniform(c->spinLimit);
+  return us >= 42949672u ? 0xffffffffu : 100u * us;
+}
+__device__ __forceinline__ bool wsElapsedOver(uint32_t t0, uint32_t budget) {
+  uint32_t dt = (uint32_t)__builtin_amdgcn_s_memrealtime() - t0;
+  asm volatile("" : "+s"(dt));
+  return dt > budget;
+}
+
 __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
 #if GSDR_WS_WAITS
   const unsigned long long t0w = __builtin_amdgcn_s_memtime();
@@ -184,26 +198,26 @@ __device__ __forceinline__ void wsWait(WsCtl* c, int* p, int target) {
     // the budget is wall clock (s_memrealtime: the constant 100 MHz counter), so a wave that is merely
     // slowed - other kernels or processes on its CU, a context switch - never counts as a hang (r06,
     // VERDICT r05 weak 2); only a hand-off that has not come in spinLimit microseconds aborts
-    const uint64_t budget = 100ull * (uint32_t)waveUniform(c->spinLimit);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t budget = wsBudgetTicks(c);
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
     for (;;) {
       if (GSDR_WS_SLEEP > 0) __builtin_amdgcn_s_sleep(GSDR_WS_SLEEP);
       const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const int ab = __hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (waveUniform(v) >= target || waveUniform(ab)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > budget) {
+      if (wsElapsedOver(t0, budget)) {
         wsRaiseAbort(c);
         break;
       }
     }
   }
 #else
-  const uint64_t budget = 100ull * (uint32_t)waveUniform(c->spinLimit), t0 = __builtin_amdgcn_s_memrealtime();
+  const uint32_t budget = wsBudgetTicks(c), t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
   for (;;) {
     const int v = waveUniform(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (v >= target) break;
     if (waveUniform(__hip_atomic_load(&c->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > budget) {
+    if (wsElapsedOver(t0, budget)) {
       wsRaiseAbort(c);
       break;
     }
@@ -286,13 +300,22 @@ struct I8WsWindow {
   uint32_t e[G];  // the next dword
 };
 
+// A 64-bit value clamped to [0, cap] with 32-bit compares only: gfx9 has no scalar 64-bit ordered compare,
+// so `x < cap` on int64 becomes a VALU v_cmp whose mask the scalar code then waits for - behind the consumer
+// wave's MFMAs on the same SIMD (r06: two such per tile cost the C5 launch 40 us).
+__device__ __forceinline__ int wsClampI64(int64_t x, int cap) {
+  int hi = (int)(x >> 32);
+  uint32_t lo = (uint32_t)x;
+  asm("" : "+s"(hi), "+s"(lo));  // opaque halves: LLVM would fold `hi < 0` back into a 64-bit compare
+  return hi < 0 ? 0 : (hi > 0 || lo > (uint32_t)cap) ? cap : (int)lo;
+}
+
 __device__ __forceinline__ i4v wsI8TileRsrc(const I8DecArgs& a, int tile, bool valid) {
   const int64_t first = (int64_t)tile * kCfTileOut * a.D * 2;  // bytes from iq4
   const int64_t total = (2 * a.nIn + a.sub + 3) & ~(int64_t)3;  // whole dwords holding input bytes
   // clamped at 0 (r06): a tile index past the input must give an empty range, never a
   // negative num_records, which as uint32 would switch the range check off
-  const int64_t left = valid && total > first ? total - first : 0;
-  const int64_t bytes = left < 0x7fffffff ? left : 0x7fffffff;
+  const int bytes = valid ? wsClampI64(total - first, 0x7fffffff) : 0;
   const uint64_t base = reinterpret_cast<uint64_t>(a.iq4 + first);
   i4v r;
   r.x = waveUniform((int)(uint32_t)base);
@@ -342,30 +365,45 @@ __device__ __forceinline__ void wsI8DrainWindows(I8WsWindow<G>& a, I8WsWindow<G>
 // C5's RF filter: 1e-20 .. 1e-8 of the largest), so an output whose window has non-zero samples ONLY under
 // such taps - at a zero-padded stream start, after an exact-zero gap - misses the 1e-6 sum|h||x| bound.
 // Such a window's samples under every other tap are zero, i.e. the tile window holds a long run of exact
-// complex zeros. A wave flags its part of the window when two consecutive 8-sample units of its 64 are all
-// zero (I = Q = 0; units past Wl or past the input's end excluded): any zero run of >= 31 samples is caught (>= 3 whole units, two
-// of them in one wave's 64), and the violating runs are ~T long. Flagged tiles are computed in the direct
-// fp32 form by the consumers (wsI8DirectOutput). An adversarial comb - non-zero samples only where a
-// windowed sinc has its zeros - is not a run and stays uncaught. Cost: 3 VALU per unit.
-#ifndef GSDR_WS_ZALT  // A/B builds only (r06 guard cost): 1 = validity by Wl alone, 2 = no zhist bit,
-                      // 4 = the zero bits computed, the run test not
-#define GSDR_WS_ZALT 0
-#endif
+// complex zeros. A wave flags its part of the window when two adjacent 8-sample units of its 64 are all
+// zero (I = Q = 0; units past Wl or past the input's end excluded; wsI8ZeroPair): any zero run of >= 39
+// samples is caught, and the violating runs are ~T long. Flagged tiles are computed in the direct form (the
+// 8-way kernel's consumers, wsI8DirectOutput; the 4-way kernel's producers, fir_i8_ws4.hip). An adversarial
+// comb - non-zero samples only where a windowed sinc has its zeros - is not a run and stays uncaught
+// (DESIGN.md 9). Cost: ~6 VALU per unit, one ballot per tile.
 #ifndef GSDR_WS_ZGUARD  // A/B builds only: bit 0 the producers' zero runs, bit 1 the 4-way consumers' flag reads
 #define GSDR_WS_ZGUARD 3
 #endif
-// Per unit: bit j of the thread's mask when unit g = ptid + kWsPThreads j is all zero (and valid); per tile,
-// once: a pair of adjacent units (neighbouring lanes, one DPP wave shift) in any lane. (r06: a ballot per
-// unit inside the conversion loop cost the C5 launch 35 us of its 147 - the scalar mask chain serialised the
-// loop; this form is ~3 VALU per unit and 4 instructions per tile.)
-__device__ __forceinline__ uint32_t wsI8ZeroBit(const uint32_t (&words)[4], bool valid, int j) {
-  if (!(GSDR_WS_ZGUARD & 1)) return 0u;
-  return (valid && (words[0] | words[1] | words[2] | words[3]) == 0u) ? (1u << j) : 0u;
+// The zero-run test in VALU arithmetic only: per unit, o = the OR of its four words; the pair (unit, next
+// unit) is all zero when o | o(neighbouring lane) is 0 (one DPP wave shift); invalid pairs - a unit or its
+// neighbour past the input, and lanes 0 and 63 (the pair that would cross the wave, whichever way the shift
+// runs) - are OR-ed with all ones; the thread keeps the minimum, and one ballot per tile tells whether any
+// pair was zero. Any zero run of >= 39 samples holds 4 whole units, 3 pairs, one of them tested. (r06: the same test with a compare per
+// unit - VALU writes of VCC, consumed by SALU - cost the C5 launch 40 us of its 145; this form ~3.)
+__device__ __forceinline__ uint32_t wsI8ZeroPair(const uint32_t (&words)[4], int g, int Wz, uint32_t edge) {
+  const uint32_t o = words[0] | words[1] | words[2] | words[3];
+  const uint32_t on = (uint32_t)__builtin_amdgcn_mov_dpp((int)o, 0x130, 0xf, 0xf, true);  // wave_shl:1
+  const uint32_t invalid = (uint32_t)((Wz - g - 2) >> 31) | edge;
+  return o | on | invalid;
 }
-__device__ __forceinline__ bool wsI8ZeroRun(uint32_t zb) {
-  if (!(GSDR_WS_ZGUARD & 1)) return false;
-  const uint32_t nb = (uint32_t)__builtin_amdgcn_mov_dpp((int)zb, 0x130, 0xf, 0xf, true);  // wave_shl:1
-  return __ballot((zb & nb) != 0u) != 0;
+// The wave's minimum in lane 63, DPP only (row shifts, then the row broadcasts): no VALU -> SALU hand-off.
+template <int CTRL, int ROWS = 0xf, int BANKS = 0xf>
+__device__ __forceinline__ uint32_t wsDppMinStep(uint32_t v) {
+  return min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROWS, BANKS, false));
+}
+__device__ __forceinline__ uint32_t wsWaveMinLane63(uint32_t v) {
+  v = wsDppMinStep<0x111>(v);            // row_shr:1
+  v = wsDppMinStep<0x112>(v);            // row_shr:2
+  v = wsDppMinStep<0x113>(v);            // row_shr:3
+  v = wsDppMinStep<0x114, 0xf, 0xe>(v);  // row_shr:4
+  v = wsDppMinStep<0x118, 0xf, 0xc>(v);  // row_shr:8 (lane 15 of each row: the row's minimum)
+  v = wsDppMinStep<0x142, 0xa, 0xf>(v);  // row_bcast:15
+  return wsDppMinStep<0x143, 0xc, 0xf>(v);  // row_bcast:31
+}
+// The tile's zero-run flag of this wave (1 / 0, valid in lane 63) from the threads' pair minima.
+__device__ __forceinline__ uint32_t wsI8ZeroRunLane63(uint32_t zmin) {
+  if (!(GSDR_WS_ZGUARD & 1)) return 0u;
+  return 1u - min(wsWaveMinLane63(zmin), 1u);
 }
 
 // zero-window flags of plane set `set` (the producer waves' zflag words, read after planesFull)
@@ -412,13 +450,15 @@ struct NoPre {
 // NS plane sets: tile i goes to set i % NS once the consumers are done with tile i - NS. Q8: int8 planes
 // (the 4-way kernel's int8 x int8 MFMA form): the 8 samples of a group are one 8-byte half of a 16-byte
 // plane slot, slot g / 2 (padded like the f16 units), half g % 2.
-// Returns whether this wave's part of the window holds a zero run (the zero-window guard, wsI8ZeroRun).
+// Returns this wave's zero-run flag of the tile (the zero-window guard) in lane 63: 1 when its part of the
+// window holds a zero run. (Kept in a VGPR: a branch on it right away would wait for the VALU - r06: a ballot
+// per tile, a VALU -> SALU hand-off behind the consumer's MFMAs on the SIMD, cost the C5 launch 40 us; lane 63
+// writes the flags with plain LDS stores, and the 4-way kernel reads the flag a tile later.)
 template <int G, int NC = kCfWaves, int NS = 2, bool Q8 = false, typename Pre = NoPre>
-// zhist (the 4-way kernel's fused chain): a flagged tile's bit (block-local index mod 64), set before the
-// planes are handed over - so before the consumers write the tile's AM samples to the ring.
-__device__ __forceinline__ bool wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
+// zlane (the 4-way kernel): the threads' pair minima go to LDS instead of a flag per wave (see below).
+__device__ __forceinline__ uint32_t wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
                                                  int i, int ptid, I8WsWindow<G>& wCur, const Pre& pre = Pre{},
-                                                 unsigned long long* st = nullptr, int* zhist = nullptr) {
+                                                 unsigned long long* st = nullptr, uint32_t* zlane = nullptr) {
   const int lane = ptid & (kWave - 1);
   const int set = i % NS;
 #if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
@@ -447,10 +487,10 @@ __device__ __forceinline__ bool wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 #endif
   int8_t* planes = smem + set * 2 * a.planeStride;
   const i4v rsrc2 = wsI8TileRsrc(a, tile + 2, i + 2 < n);
-  uint32_t zb = 0;
+  uint32_t zmin = 0xffffffffu;
+  const uint32_t edge = 0u - (uint32_t)(((lane + 1) >> 6) | ((64 - lane) >> 6));  // lanes 0, 63
   // units wholly inside the input: the last tile's window runs past it (zeros, out of range), not a run
-  const int64_t inU = (a.nIn - (int64_t)tile * kCfTileOut * a.D) >> 3;
-  const int Wz = inU < Wl ? (int)(inU > 0 ? inU : 0) : Wl;
+  const int Wz = wsClampI64((a.nIn - (int64_t)tile * kCfTileOut * a.D) >> 3, Wl);
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     const int g = ptid + kWsPThreads * j;
@@ -458,7 +498,7 @@ __device__ __forceinline__ bool wsI8ProducerTile(const I8DecArgs& a, int Wl, int
                                __builtin_amdgcn_alignbyte(wCur.q[j].z, wCur.q[j].y, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.q[j].w, wCur.q[j].z, a.sub),
                                __builtin_amdgcn_alignbyte(wCur.e[j], wCur.q[j].w, a.sub)};
-    zb |= wsI8ZeroBit(words, (GSDR_WS_ZALT & 1) ? g < Wl : g < Wz, j);
+    if (GSDR_WS_ZGUARD & 1) zmin = min(zmin, wsI8ZeroPair(words, g, Wz, edge));
     if constexpr (Q8) {
       uint2 iu, qu;
       int8IqToI8Units(words, iu, qu);
@@ -490,11 +530,15 @@ __device__ __forceinline__ bool wsI8ProducerTile(const I8DecArgs& a, int Wl, int
     wsI8LoadGroup<G>(rsrc2, Wl, ptid, j, wCur);
   }
   if (ptid == 0) c->mode[set] = 0;
-  if (GSDR_WS_ZALT & 4) asm volatile("" ::"v"(zb));
-  const bool zrun = (GSDR_WS_ZALT & 4) ? false : wsI8ZeroRun(zb);
-  if (lane == 0) c->zflag[set][ptid >> 6] = zrun ? 1 : 0;  // published by the planesFull release
-  if (!(GSDR_WS_ZALT & 2) && zhist != nullptr && zrun && lane == 0)
-    __hip_atomic_fetch_or(&zhist[(i >> 5) & 1], 1 << (i & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  uint32_t zflag = 0;
+  if (zlane != nullptr) {
+    // 4-way kernel: every lane's pair minimum to LDS ([set][lane][producer wave]: one ds_read_b128 per consumer
+    // lane gathers the four waves'), reduced by the consumer waves - no dependent chain in the producer
+    zlane[set * kWsPThreads + 4 * lane + (ptid >> 6)] = zmin;
+  } else {
+    zflag = wsI8ZeroRunLane63(zmin);
+    if (lane == kWave - 1) c->zflag[set][ptid >> 6] = (int)zflag;  // published by the planesFull release
+  }
   wsSignal(&c->planesFull[set], lane);
 #if GSDR_WS_WAITS || defined(GSDR_W4_STAMPS)
   if (st) st[3] += __builtin_amdgcn_s_memtime() - t0s;
@@ -502,7 +546,7 @@ __device__ __forceinline__ bool wsI8ProducerTile(const I8DecArgs& a, int Wl, int
 #ifdef W4TR
   if (ptid < kWave) { W4TR(1, i, 3) }
 #endif
-  return zrun;
+  return zflag;
 }
 
 
