@@ -561,6 +561,9 @@ __device__ __forceinline__ uint32_t wsI8ProducerTile(const I8DecArgs& a, int Wl,
 // producers, who feed the matrix cores, the bottleneck: C5 0.18 -> 0.71 ms per step).
 // The lead tile (the previous block's last, computed for the ring only) has no outputs here.
 constexpr int kAudioTapsPerLane = kAudioMaxTaps / 8;
+#ifndef GSDR_AUDIO_ACC  // packed partial sums per audio window (A/B: 2 or 4)
+#define GSDR_AUDIO_ACC 2
+#endif
 #ifndef GSDR_AUDIO_ROTATE
 #define GSDR_AUDIO_ROTATE 1
 #endif
@@ -678,13 +681,26 @@ __device__ __forceinline__ void wsAudioTile(const I8DecArgs& a, const float* rin
 #pragma unroll
         for (int k = 0; k < kAudioTapsPerLane / 2; ++k) xv[k] = f2{w[16 * k], w[16 * k + 8]};
         asm volatile("" ::: "memory");
-        f2 a0 = f2{0.0f, 0.0f}, a1 = f2{0.0f, 0.0f};
+        if (GSDR_AUDIO_ACC == 4) {  // four packed partial sums: dependent FMA chains of 4, not 8
+          f2 a0 = f2{0.0f, 0.0f}, a1 = a0, a2 = a0, a3 = a0;
 #pragma unroll
-        for (int k = 0; k < kAudioTapsPerLane / 2; k += 2) {
-          a0 = __builtin_elementwise_fma(f2{ht[2 * k], ht[2 * k + 1]}, xv[k], a0);
-          a1 = __builtin_elementwise_fma(f2{ht[2 * k + 2], ht[2 * k + 3]}, xv[k + 1], a1);
+          for (int k = 0; k < kAudioTapsPerLane / 2; k += 4) {
+            a0 = __builtin_elementwise_fma(f2{ht[2 * k], ht[2 * k + 1]}, xv[k], a0);
+            a1 = __builtin_elementwise_fma(f2{ht[2 * k + 2], ht[2 * k + 3]}, xv[k + 1], a1);
+            a2 = __builtin_elementwise_fma(f2{ht[2 * k + 4], ht[2 * k + 5]}, xv[k + 2], a2);
+            a3 = __builtin_elementwise_fma(f2{ht[2 * k + 6], ht[2 * k + 7]}, xv[k + 3], a3);
+          }
+          const f2 b0 = a0 + a2, b1 = a1 + a3;
+          s = (b0.x + b0.y) + (b1.x + b1.y);
+        } else {
+          f2 a0 = f2{0.0f, 0.0f}, a1 = f2{0.0f, 0.0f};
+#pragma unroll
+          for (int k = 0; k < kAudioTapsPerLane / 2; k += 2) {
+            a0 = __builtin_elementwise_fma(f2{ht[2 * k], ht[2 * k + 1]}, xv[k], a0);
+            a1 = __builtin_elementwise_fma(f2{ht[2 * k + 2], ht[2 * k + 3]}, xv[k + 1], a1);
+          }
+          s = (a0.x + a0.y) + (a1.x + a1.y);
         }
-        s = (a0.x + a0.y) + (a1.x + a1.y);
       } else {  // windows reaching into the history (the launch's first outputs)
         // buffer loads (range-checked): a pointer select between the ring and the history would
         // compile to FLAT loads
