@@ -163,7 +163,7 @@ __device__ __forceinline__ void w4RingWrite(float* ring, int j, int tid, const f
 // wrote it, before any window reads it. (The wait in w4PatchRing is then already satisfied.)
 __device__ __forceinline__ float w4DirectValue(const I8DecArgs& a, int64_t k, int epi, float& im) {
   double si, sq;
-  wsI8DirectSums(a.iq4 + a.sub, a.taps, a.T, a.D, k, si, sq);
+  wsI8DirectSums<1>(a.iq4 + a.sub, a.taps, a.T, a.D, k, si, sq);
   si *= 1.0 / 127.0;
   sq *= 1.0 / 127.0;
   im = (float)sq;

@@ -413,13 +413,16 @@ __device__ __forceinline__ bool wsI8Zflag(const WsCtl* c, int set) {
 
 // Direct form of int8 IQ output k (the guard's tiles): sum_j h_j I'_kD+j and sum_j h_j Q'_kD+j with
 // x' = max(x, -127), accumulated in double (rare tiles; a sequential fp32 sum of ~1 000 products can
-// reach 1e-6 of sum|h||x|, tests/test_mfma_guard.py). Not unrolled: little code, few registers.
+// reach 1e-6 of sum|h||x|, tests/test_mfma_guard.py). U: unroll; 1 in both kernels (r06: 4 or 8 in the 4-way
+// kernel's producers would keep more tap loads in flight - a flagged tile costs its block ~180 us - but spilled
+// SGPRs of the C5 kernel; in the 8-way kernel's consumers, VGPRs).
+template <int U = 1>
 __device__ __forceinline__ void wsI8DirectSums(const int8_t* iq, const float* taps, int T, int D, int64_t k, double& si,
                                                double& sq) {
   const int8_t* p = iq + 2 * k * D;
   si = 0.0;
   sq = 0.0;
-#pragma unroll 1
+#pragma unroll U
   for (int j = 0; j < T; ++j) {
     const double h = taps[j];
     si = fma(h, (double)max((int)p[2 * j], -127), si);
