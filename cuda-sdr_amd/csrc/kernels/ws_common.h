@@ -173,9 +173,8 @@ __device__ __forceinline__ void wsRaiseAbort(WsCtl* c) {
 }
 
 // The hand-off budget in s_memrealtime ticks (100 MHz), 32 bits: the elapsed time is compared modulo 2^32
-// (42.9 s), so a budget above that saturates. 32-bit scalar compares only - a 64-bit ordered compare is a VALU
-// v_cmp on gfx9, and its mask reaches the scalar branch only after the VALU queue behind the SIMD's MFMAs
-// drains (r06: the C5 launch's producer waves paid that per tile; see wsClampI64).
+// (42.9 s), so a budget above that saturates. 32-bit scalar compares only: a 64-bit ordered compare is a VALU
+// v_cmp on gfx9, whose mask the scalar branch must wait for (a VALU -> SALU hand-off; see wsClampI64).
 __device__ __forceinline__ uint32_t wsBudgetTicks(const WsCtl* c) {
   const uint32_t us = (uint32_t)waveUniform(c->spinLimit);
   return us >= 42949672u ? 0xffffffffu : 100u * us;
@@ -301,8 +300,8 @@ struct I8WsWindow {
 };
 
 // A 64-bit value clamped to [0, cap] with 32-bit compares only: gfx9 has no scalar 64-bit ordered compare,
-// so `x < cap` on int64 becomes a VALU v_cmp whose mask the scalar code then waits for - behind the consumer
-// wave's MFMAs on the same SIMD (r06: two such per tile cost the C5 launch 40 us).
+// so `x < cap` on int64 becomes a VALU v_cmp whose mask the scalar code then waits for. (r06: removed from the
+// producers' per-tile range math while chasing the zero-window guard's cost - measured neutral by itself.)
 __device__ __forceinline__ int wsClampI64(int64_t x, int cap) {
   int hi = (int)(x >> 32);
   uint32_t lo = (uint32_t)x;
@@ -377,9 +376,10 @@ __device__ __forceinline__ void wsI8DrainWindows(I8WsWindow<G>& a, I8WsWindow<G>
 // The zero-run test in VALU arithmetic only: per unit, o = the OR of its four words; the pair (unit, next
 // unit) is all zero when o | o(neighbouring lane) is 0 (one DPP wave shift); invalid pairs - a unit or its
 // neighbour past the input, and lanes 0 and 63 (the pair that would cross the wave, whichever way the shift
-// runs) - are OR-ed with all ones; the thread keeps the minimum, and one ballot per tile tells whether any
-// pair was zero. Any zero run of >= 39 samples holds 4 whole units, 3 pairs, one of them tested. (r06: the same test with a compare per
-// unit - VALU writes of VCC, consumed by SALU - cost the C5 launch 40 us of its 145; this form ~3.)
+// runs) - are OR-ed with all ones; the thread keeps the minimum. Any zero run of >= 39 samples holds 4 whole
+// units, 3 pairs, one of them tested. The reduction over the threads is the consumers' in the 4-way kernel
+// (r06: every form that finished it in the producer - a compare per unit, a ballot or a DPP min chain per tile
+// - cost the C5 launch 35-50 us of its 145; this form + the consumer reduction 3.5 us).
 __device__ __forceinline__ uint32_t wsI8ZeroPair(const uint32_t (&words)[4], int g, int Wz, uint32_t edge) {
   const uint32_t o = words[0] | words[1] | words[2] | words[3];
   const uint32_t on = (uint32_t)__builtin_amdgcn_mov_dpp((int)o, 0x130, 0xf, 0xf, true);  // wave_shl:1
@@ -454,9 +454,8 @@ struct NoPre {
 // (the 4-way kernel's int8 x int8 MFMA form): the 8 samples of a group are one 8-byte half of a 16-byte
 // plane slot, slot g / 2 (padded like the f16 units), half g % 2.
 // Returns this wave's zero-run flag of the tile (the zero-window guard) in lane 63: 1 when its part of the
-// window holds a zero run. (Kept in a VGPR: a branch on it right away would wait for the VALU - r06: a ballot
-// per tile, a VALU -> SALU hand-off behind the consumer's MFMAs on the SIMD, cost the C5 launch 40 us; lane 63
-// writes the flags with plain LDS stores, and the 4-way kernel reads the flag a tile later.)
+// window holds a zero run - the 8-way kernel's form (lane 63 stores it); with zlane (the 4-way kernel) 0: the
+// per-lane minima go to LDS for the consumers to reduce.
 template <int G, int NC = kCfWaves, int NS = 2, bool Q8 = false, typename Pre = NoPre>
 // zlane (the 4-way kernel): the threads' pair minima go to LDS instead of a flag per wave (see below).
 __device__ __forceinline__ uint32_t wsI8ProducerTile(const I8DecArgs& a, int Wl, int8_t* smem, WsCtl* c, int n, int tile,
